@@ -1,0 +1,241 @@
+"""ctypes binding of the MI355X engine (include/globalign_amd.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+GPU is visible, every entry point raises.  The shared library is built
+in-tree by ``__graft_entry__.build()`` (``make -C globalign_amd/csrc``).
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libglobalign_amd.so")
+
+GA_FILL_TRACEBACK = 1
+GA_FILL_FULL = 2
+GA_TB_OK = 0
+GA_TB_INDEX_ERROR = 1
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class GaCosts(C.Structure):
+    _fields_ = [
+        ("K", C.c_int32),
+        ("sub", C.POINTER(C.c_int32)),
+        ("gap_h", C.POINTER(C.c_int32)),
+        ("gap_v", C.POINTER(C.c_int32)),
+        ("gap_open", C.c_int32),
+        ("max_cost", C.c_int32),
+    ]
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+# every symbol include/globalign_amd.h declares (tests check the exports)
+EXPORTS = [
+    "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill",
+    "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_fill_launch",
+    "ga_slab_fill_finish", "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms",
+]
+
+
+def load_library():
+    """Load libglobalign_amd.so (raises ImportError when it has not been built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        i64, i32, vp = C.c_int64, C.c_int32, C.c_void_p
+        p32, pu32, pi64 = C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.POINTER(C.c_int64)
+        L.ga_last_error.restype = C.c_char_p
+        L.ga_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.ga_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+        L.ga_ctx_destroy.argtypes = [vp]
+        L.ga_ctx_destroy.restype = None
+        L.ga_problem_set.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), p32, p32]
+        L.ga_problem_fill.argtypes = [vp, i32, pi64, p32]
+        L.ga_problem_traceback.argtypes = [vp, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i64,
+                                           pi64, p32]
+        L.ga_problem_align.argtypes = [vp, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i64,
+                                       pi64, p32, pi64]
+        L.ga_problem_set_slab.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), i64, i64]
+        L.ga_slab_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
+        L.ga_slab_fill_launch.argtypes = [vp, i32]
+        L.ga_slab_fill_finish.argtypes = [vp, pi64]
+        L.ga_stream_wait_ge.argtypes = [vp, vp, C.c_uint32]
+        L.ga_stream_write.argtypes = [vp, vp, C.c_uint32]
+        L.ga_ctx_stream.argtypes = [vp]
+        L.ga_ctx_stream.restype = vp
+        L.ga_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        _lib = L
+        return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = _lib.ga_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(msg)
+        raise EngineError(f"globalign_amd engine error {rc}: {msg}")
+
+
+def device_count():
+    L = load_library()
+    n = C.c_int(0)
+    _check(L.ga_device_count(C.byref(n)))
+    return n.value
+
+
+class CostTables:
+    """Integer view of a costing dict: codes follow the dict's key order."""
+
+    def __init__(self, costing_mat, gap_open_cost):
+        self.keys = list(costing_mat.keys())
+        if "-" not in costing_mat:
+            raise KeyError("-")
+        self.code = {k: i for i, k in enumerate(self.keys)}
+        K = len(self.keys)
+        self.sub = np.array([[int(costing_mat[x][y]) for y in self.keys] for x in self.keys], dtype=np.int32).reshape(-1)
+        self.gap_h = np.array([int(costing_mat["-"][y]) for y in self.keys], dtype=np.int32)
+        self.gap_v = np.array([int(costing_mat[x]["-"]) for x in self.keys], dtype=np.int32)
+        self.max_cost = int(max(max(row.values()) for row in costing_mat.values()))
+        self.gap_open = int(gap_open_cost)
+        self.K = K
+        p32 = C.POINTER(C.c_int32)
+        self.struct = GaCosts(K, self.sub.ctypes.data_as(p32), self.gap_h.ctypes.data_as(p32),
+                              self.gap_v.ctypes.data_as(p32), self.gap_open, self.max_cost)
+
+    def codes(self, seq):
+        code = self.code
+        return bytes(code[ch] for ch in seq)
+
+
+class Engine:
+    """One HIP device context (ga_ctx)."""
+
+    def __init__(self, device=0):
+        L = load_library()
+        if device_count() < 1:
+            raise EngineError("no HIP device visible: the globalign_amd engine runs on MI355X (gfx950) only")
+        self._L = L
+        h = C.c_void_p()
+        _check(L.ga_ctx_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = device
+        self.m = self.n = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ga_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- problem -------------------------------------------------------------
+    def load(self, a_codes, b_codes, tables, row0=None, col0=None):
+        p32 = C.POINTER(C.c_int32)
+        r0 = c0 = None
+        if row0 is not None:
+            self._row0 = np.ascontiguousarray(row0, dtype=np.int32).reshape(-1)
+            self._col0 = np.ascontiguousarray(col0, dtype=np.int32).reshape(-1)
+            r0, c0 = self._row0.ctypes.data_as(p32), self._col0.ctypes.data_as(p32)
+        self._tables = tables
+        _check(self._L.ga_problem_set(self._h, a_codes, len(a_codes), b_codes, len(b_codes), C.byref(tables.struct),
+                                      r0, c0))
+        self.m, self.n = len(a_codes), len(b_codes)
+
+    def fill(self, traceback=False, full=False):
+        flags = (GA_FILL_TRACEBACK if traceback else 0) | (GA_FILL_FULL if full else 0)
+        cost = C.c_int64(0)
+        out = None
+        ptr = None
+        if full:
+            out = np.zeros((self.m + 1, self.n + 1, 3), dtype=np.int32)
+            ptr = out.ctypes.data_as(C.POINTER(C.c_int32))
+        _check(self._L.ga_problem_fill(self._h, flags, C.byref(cost), ptr))
+        return cost.value, out
+
+    def _tb_call(self, fn, mt_words, a_chr, b_chr, extra=()):
+        mt = np.ascontiguousarray(mt_words, dtype=np.uint32).copy()
+        cap = self.m + self.n + 2
+        oa, om, ob = C.create_string_buffer(cap), C.create_string_buffer(cap), C.create_string_buffer(cap)
+        ln, st = C.c_int64(0), C.c_int32(0)
+        _check(fn(self._h, mt.ctypes.data_as(C.POINTER(C.c_uint32)), a_chr.encode(), b_chr.encode(), oa, om, ob, cap,
+                  C.byref(ln), C.byref(st), *extra))
+        L = ln.value
+        strings = (oa.raw[:L].decode(), om.raw[:L].decode(), ob.raw[:L].decode())
+        return strings, st.value, mt
+
+    def traceback(self, mt_words, a_chr, b_chr):
+        """-> ((seq_1_aligned, middle, seq_2_aligned), status, mt_words_after)"""
+        return self._tb_call(self._L.ga_problem_traceback, mt_words, a_chr, b_chr)
+
+    def align(self, mt_words, a_chr, b_chr):
+        """fill + traceback -> (cost, strings, status, mt_words_after)"""
+        cost = C.c_int64(0)
+        strings, st, mt = self._tb_call(self._L.ga_problem_align, mt_words, a_chr, b_chr, (C.byref(cost),))
+        return cost.value, strings, st, mt
+
+    def kernel_ms(self):
+        f, w = C.c_float(0), C.c_float(0)
+        _check(self._L.ga_last_kernel_ms(self._h, C.byref(f), C.byref(w)))
+        return f.value, w.value
+
+    # -- slabs (multi-GPU) ---------------------------------------------------
+    def load_slab(self, a_codes, b_codes, tables, col_begin, col_end):
+        self._tables = tables
+        _check(self._L.ga_problem_set_slab(self._h, a_codes, len(a_codes), b_codes, len(b_codes),
+                                           C.byref(tables.struct), int(col_begin), int(col_end)))
+        self.m, self.n = len(a_codes), int(col_end - col_begin)
+
+    def slab_buffers(self):
+        vp = C.c_void_p
+        hi, hip_, ho, hop = vp(), vp(), vp(), vp()
+        _check(self._L.ga_slab_buffers(self._h, C.byref(hi), C.byref(hip_), C.byref(ho), C.byref(hop)))
+        return hi.value, hip_.value, ho.value, hop.value
+
+    def slab_launch(self, traceback=False):
+        _check(self._L.ga_slab_fill_launch(self._h, GA_FILL_TRACEBACK if traceback else 0))
+
+    def slab_finish(self):
+        cost = C.c_int64(0)
+        _check(self._L.ga_slab_fill_finish(self._h, C.byref(cost)))
+        return cost.value
+
+    def stream(self):
+        return self._L.ga_ctx_stream(self._h)
+
+    def stream_wait_ge(self, stream, prog_ptr, value):
+        _check(self._L.ga_stream_wait_ge(C.c_void_p(stream), C.c_void_p(prog_ptr), int(value)))
+
+    def stream_write(self, stream, prog_ptr, value):
+        _check(self._L.ga_stream_write(C.c_void_p(stream), C.c_void_p(prog_ptr), int(value)))
+
+
+_default = {}
+_default_lock = threading.Lock()
+
+
+def default_engine(device=0):
+    """Process-wide engine per device (contexts are not thread-safe: one per thread)."""
+    key = (device, threading.get_ident())
+    with _default_lock:
+        eng = _default.get(key)
+        if eng is None:
+            eng = Engine(device)
+            _default[key] = eng
+        return eng

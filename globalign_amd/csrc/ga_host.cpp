@@ -1,0 +1,568 @@
+// ga_host.cpp -- host side of the C ABI declared in include/globalign_amd.h.
+//
+// Owns device memory and the HIP stream of one context, runs the kernels of
+// ga_kernels.hip, and does the two pieces of the traceback that are
+// inherently host-side in the reference's semantics:
+//   * the tie-break table: the reference draws 18 random.choice values per
+//     dispatched traceback step from CPython's global MT19937
+//     (globaligner.py:598-672); we emulate genrand_uint32 and
+//     _randbelow_with_getrandbits exactly, starting from random.getstate(),
+//     while the device fill runs;
+//   * string assembly from the walk's per-step levels (take_* :688-753,
+//     the i==0 / j==0 tails :542-581 and the final reverse :584-586).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/globalign_amd.h"
+#include "ga_device.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(GA_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+// ------------------------------------------------------------------ buffers
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool uncached = false;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = uncached ? hipExtMallocWithFlags(&p, want, hipDeviceMallocUncached) : hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ------------------------------------------------------------------ CPython MT19937
+constexpr int MTN = 624, MTM = 397;
+
+struct PyMT {
+    uint32_t mt[MTN];
+    int mti;
+    void twist() {
+        static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+        int kk = 0;
+        uint32_t y;
+        for (; kk < MTN - MTM; kk++) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + MTM] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        for (; kk < MTN - 1; kk++) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + (MTM - MTN)] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        y = (mt[MTN - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+        mt[MTN - 1] = mt[MTM - 1] ^ (y >> 1) ^ mag01[y & 1u];
+        mti = 0;
+    }
+    inline uint32_t next() {
+        if (mti >= MTN) twist();
+        uint32_t y = mt[mti++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+    // random.choice(seq of len n) for n in {2,3}: getrandbits(2) with rejection
+    inline unsigned below(unsigned n) {
+        unsigned r;
+        do { r = next() >> 30; } while (r >= n);
+        return r;
+    }
+};
+
+constexpr int SNAP = 1024;  // MT snapshots every SNAP dispatches
+
+// One dispatcher call = 18 draws of sizes [3,2,2,2,3,2,2,2,3] x {match, mismatch}.
+// Only draws 0-3 (match) and 9-12 (mismatch) can decide a move; pack them.
+inline uint16_t dispatch_bits(PyMT& g) {
+    static const unsigned sizes[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
+    unsigned r[18];
+    for (int d = 0; d < 18; d++) r[d] = g.below(sizes[d]);
+    return (uint16_t)(r[0] | (r[1] << 2) | (r[2] << 3) | (r[3] << 4) | (r[9] << 5) | (r[10] << 7) | (r[11] << 8) |
+                      (r[12] << 9));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ context
+struct ga_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // problem
+    bool loaded = false, custom = false, filled_tb = false;
+    int64_t m = 0, n = 0;      // local problem (slab: n = local columns)
+    int64_t n_global = 0, col0 = 0;
+    int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
+    int nstripes = 0, nslabs = 0, TC = 0;
+    int64_t GV_m = 0, GH_n = 0;
+    std::vector<uint8_t> h_a, h_b;
+    // device buffers
+    DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng,
+        ops, result;
+    DevBuf halo_in{nullptr, 0, true}, prog{nullptr, 0, true};
+    bool slab = false;
+    float fill_ms = 0.f, walk_ms = 0.f;
+};
+
+namespace {
+
+int check_ctx(ga_ctx* c) {
+    if (!c) return fail(GA_E_ARG, "null context");
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return fail(GA_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    return GA_OK;
+}
+
+int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
+                 const int32_t* row0, const int32_t* col0, int64_t cb, int64_t ce) {
+    if (!a || !b_all || !cs || !cs->sub || !cs->gap_h || !cs->gap_v) return fail(GA_E_ARG, "null argument");
+    if (m < 1 || n_all < 1) return fail(GA_E_ARG, "sequences must be non-empty");
+    if (cb < 0 || ce > n_all || ce <= cb) return fail(GA_E_ARG, "bad column slab");
+    const int K = cs->K;
+    if (K < 1 || K > 255) return fail(GA_E_ARG, "alphabet size K must be in [1,255]");
+    if (cs->gap_open < 0) return fail(GA_E_ARG, "gap_open cost must be >= 0");
+    for (int64_t i = 0; i < m; i++)
+        if (a[i] >= K) return fail(GA_E_ARG, "seq_1 code out of range");
+    for (int64_t j = 0; j < n_all; j++)
+        if (b_all[j] >= K) return fail(GA_E_ARG, "seq_2 code out of range");
+    // int32 range guard: every stored value, shifted or not, and
+    // every intermediate (value + o) must stay far from overflow.
+    int64_t maxabs = 0;
+    for (int q = 0; q < K * K; q++) maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->sub[q]));
+    for (int q = 0; q < K; q++) {
+        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_h[q]));
+        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_v[q]));
+    }
+    const int64_t big = ((int64_t)cs->max_cost + 1) * std::max(m, n_all);
+    int64_t bmax = std::llabs(big);
+    if (row0)
+        for (int64_t q = 0; q < 3 * (n_all + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)row0[q]));
+    if (col0)
+        for (int64_t q = 0; q < 3 * (m + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)col0[q]));
+    const int64_t bound = bmax + (m + n_all + 2) * (3 * maxabs + (int64_t)cs->gap_open);
+    if (4 * bound >= (int64_t)INT32_MAX) return fail(GA_E_RANGE, "problem exceeds the int32 score range of the device path");
+    int64_t subp_max = 0;
+    for (int x = 0; x < K; x++)
+        for (int y = 0; y < K; y++)
+            subp_max = std::max<int64_t>(subp_max,
+                                         std::llabs((long long)cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y]));
+    c->qbytes = subp_max <= 127 ? 1 : subp_max <= 32767 ? 2 : 0;
+    if (!c->qbytes) return fail(GA_E_RANGE, "substitution costs exceed the int16 query profile");
+    const int o = cs->gap_open;
+    c->CB = (o + 1) < 8 ? 1 : (o + 1) < 128 ? 2 : (o + 1) < 32768 ? 4 : 0;
+    if (!c->CB) return fail(GA_E_RANGE, "gap_open cost too large for the traceback word");
+    c->m = m;
+    c->n = ce - cb;
+    c->n_global = n_all;
+    c->col0 = cb;
+    c->K = K;
+    c->o = o;
+    c->big = (int)big;
+    c->custom = row0 != nullptr || col0 != nullptr;
+    if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
+    c->nstripes = (int)((c->n + 63) / 64);
+    c->nslabs = (c->nstripes + ga::NW - 1) / ga::NW;
+    c->h_a.assign(a, a + m);
+    c->h_b.assign(b_all, b_all + n_all);
+    HIPCHK(c->a.ensure(m));
+    HIPCHK(c->b.ensure(n_all));
+    HIPCHK(c->sub.ensure(sizeof(int) * K * K));
+    HIPCHK(c->gh.ensure(sizeof(int) * K));
+    HIPCHK(c->gv.ensure(sizeof(int) * K));
+    HIPCHK(hipMemcpyAsync(c->a.p, a, m, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->b.p, b_all, n_all, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sub.p, cs->sub, sizeof(int) * K * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->gh.p, cs->gap_h, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->gv.p, cs->gap_v, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c->bnd_row.ensure(sizeof(int) * 3 * (n_all + 1)));
+    HIPCHK(c->bnd_col.ensure(sizeof(int) * 3 * (m + 1)));
+    if (c->custom) {
+        HIPCHK(hipMemcpyAsync(c->bnd_row.p, row0, sizeof(int) * 3 * (n_all + 1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->bnd_col.p, col0, sizeof(int) * 3 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    }
+    const long long stride = m + 2 * ga::QPAD;
+    HIPCHK(c->qp.ensure((size_t)stride * K * c->qbytes));
+    HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
+    HIPCHK(c->GHp.ensure(sizeof(int) * (n_all + 1)));
+    HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
+    HIPCHK(c->left.ensure(sizeof(int2) * (m + 1)));
+    HIPCHK(c->meta.ensure(sizeof(int) * 8));
+    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
+    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
+    HIPCHK(c->out_last.ensure(sizeof(int) * 4));
+    HIPCHK(c->result.ensure(sizeof(int) * 4));
+    HIPCHK(c->ops.ensure(m + n_all + 8));
+    HIPCHK(c->rng.ensure(sizeof(uint16_t) * (m + n_all + 2)));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->loaded = true;
+    c->filled_tb = false;
+    return GA_OK;
+}
+
+// Enqueue boundary + query profile + fill.  Does not synchronise.
+int enqueue_fill(ga_ctx* c, int32_t flags) {
+    if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
+    const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
+    const bool full = (flags & GA_FILL_FULL) != 0;
+    const int64_t m = c->m, n = c->n;
+    const int spc = 16 / c->CB;
+    c->TC = (int)((m + 63 + spc - 1) / spc);
+    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->TC * 1024));
+    if (full) {
+        if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
+        HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
+    }
+    unsigned* fl = c->flags.as<unsigned>();
+    // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
+    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
+    ga::launch_qp(c->stream, c->a.as<uint8_t>(), (int)m, c->sub.as<int>(), c->gh.as<int>(), c->gv.as<int>(), c->K,
+                  c->qp.p, m + 2 * ga::QPAD, c->qbytes);
+    ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
+                        c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
+                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom);
+    ga::FillArgs p{};
+    p.qp = c->qp.p;
+    p.qp_stride = m + 2 * ga::QPAD;
+    p.b = c->b.as<uint8_t>() + c->col0;
+    p.top = c->top.as<int2>() + c->col0;
+    if (c->slab && c->col0 > 0) {
+        p.left = c->halo_in.as<int2>();
+        p.left_prog = c->prog.as<unsigned>();  // [0]: halo_in rows
+    } else {
+        p.left = c->left.as<int2>();
+        p.left_prog = nullptr;
+    }
+    p.hand = c->hand.as<int2>();
+    p.hand_prog = fl + 16;
+    p.ticket = fl;
+    p.abort_word = fl + 1;
+    p.tb = tb ? c->tb.as<uint8_t>() : nullptr;
+    p.out_last = c->out_last.as<int>();
+    p.edge_prog = c->slab ? c->prog.as<unsigned>() + 1 : nullptr;  // [1]: halo_out rows
+    p.full = full ? c->full.as<int>() : nullptr;
+    p.m = (int)m;
+    p.n = (int)n;
+    p.o = c->o;
+    p.nstripes = c->nstripes;
+    p.nslabs = c->nslabs;
+    p.TC = c->TC;
+    p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
+    p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    c->filled_tb = tb;
+    return GA_OK;
+}
+
+int finish_fill(ga_ctx* c, int64_t* cost_out, int32_t* full_out) {
+    int last[4] = {0, 0, 0, 0}, meta[2] = {0, 0};
+    unsigned abort_word = 0;
+    HIPCHK(hipMemcpyAsync(last, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(meta, c->meta.p, sizeof(int) * 2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&abort_word, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&c->fill_ms, c->ev[0], c->ev[1]));
+    if (abort_word) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+    c->GV_m = meta[0];
+    // un-shift: cost = H'(m, n) + GV(m) + GH(column)
+    int64_t gh_end = 0;
+    {
+        int v = 0;
+        HIPCHK(hipMemcpy(&v, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost));
+        gh_end = v;
+    }
+    if (cost_out) *cost_out = (int64_t)last[0] + c->GV_m + gh_end;
+    if (full_out) {
+        const int64_t m = c->m, n = c->n, W = n + 1;
+        std::vector<int> GV(m + 1), GH(n + 1);
+        HIPCHK(hipMemcpy(GV.data(), c->GVp.p, sizeof(int) * (m + 1), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(GH.data(), c->GHp.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(full_out, c->full.p, sizeof(int) * 3 * (m + 1) * W, hipMemcpyDeviceToHost));
+        std::vector<int> br(3 * (n + 1)), bc(3 * (m + 1));
+        HIPCHK(hipMemcpy(br.data(), c->bnd_row.p, sizeof(int) * br.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bc.data(), c->bnd_col.p, sizeof(int) * bc.size(), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i <= m; i++)
+            for (int64_t j = 0; j <= n; j++) {
+                int* f = full_out + 3 * (i * W + j);
+                if (i == 0) { f[0] = br[3 * j]; f[1] = br[3 * j + 1]; f[2] = br[3 * j + 2]; }
+                else if (j == 0) { f[0] = bc[3 * i]; f[1] = bc[3 * i + 1]; f[2] = bc[3 * i + 2]; }
+                else {
+                    const int sh = GV[i] + GH[j];
+                    f[0] += sh; f[1] += sh; f[2] += sh;
+                }
+            }
+    }
+    return GA_OK;
+}
+
+// Tie-break table for up to `steps` dispatches + MT snapshots every SNAP.
+void build_rng(const uint32_t* state, int64_t steps, std::vector<uint16_t>& tab, std::vector<PyMT>& snaps) {
+    PyMT g;
+    std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
+    g.mti = (int)state[MTN];
+    tab.resize(steps);
+    snaps.clear();
+    snaps.reserve(steps / SNAP + 1);
+    for (int64_t k = 0; k < steps; k++) {
+        if (k % SNAP == 0) snaps.push_back(g);
+        tab[k] = dispatch_bits(g);
+    }
+    if (steps % SNAP == 0) snaps.push_back(g);
+}
+
+void state_after(const std::vector<PyMT>& snaps, int64_t D, uint32_t* out) {
+    PyMT g = snaps[D / SNAP];
+    for (int64_t k = 0; k < D % SNAP; k++) (void)dispatch_bits(g);
+    std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
+    out[MTN] = (uint32_t)g.mti;
+}
+
+int run_walk(ga_ctx* c, const std::vector<uint16_t>& tab) {
+    HIPCHK(hipMemcpyAsync(c->rng.p, tab.data(), sizeof(uint16_t) * tab.size(), hipMemcpyHostToDevice, c->stream));
+    ga::WalkArgs w{};
+    w.tb = c->tb.as<uint8_t>();
+    w.CB = c->CB;
+    w.TC = c->TC;
+    w.a = c->a.as<uint8_t>();
+    w.b = c->b.as<uint8_t>();
+    w.bnd_row = c->bnd_row.as<int>();
+    w.bnd_col = c->bnd_col.as<int>();
+    w.rng = c->rng.as<uint16_t>();
+    w.nrng = (long long)tab.size();
+    w.m = (int)c->m;
+    w.n = (int)c->n;
+    w.o = c->o;
+    w.ops = c->ops.as<uint8_t>();
+    w.result = c->result.as<int>();
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    ga::launch_walk(c->stream, w);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    return GA_OK;
+}
+
+inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
+
+int finish_walk(ga_ctx* c, const std::vector<PyMT>& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
+                char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
+    int res[4];
+    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&c->walk_ms, c->ev[2], c->ev[3]));
+    const int64_t D = res[0];
+    const int reason = res[3];
+    std::vector<uint8_t> ops(D);
+    if (D) HIPCHK(hipMemcpy(ops.data(), c->ops.p, D, hipMemcpyDeviceToHost));
+    state_after(snaps, D, mt_state);
+    if (reason == 4) {  // IndexError in the reference
+        *tb_status = GA_TB_INDEX_ERROR;
+        *out_len = 0;
+        return GA_OK;
+    }
+    const int64_t m = c->m, n = c->n;
+    int64_t i = m, j = n, len = 0;
+    auto put = [&](char x, char y, char z) {
+        if (len < cap) { oa[len] = x; om[len] = y; ob[len] = z; }
+        len++;
+    };
+    for (int64_t k = 0; k < D; k++) {
+        const char ca = a_chr[pywrap(i - 1, m)], cbb = b_chr[pywrap(j - 1, n)];
+        if (ops[k] == 0) { put(ca, ca == cbb ? '|' : '*', cbb); i--; j--; }
+        else if (ops[k] == 1) { put('-', ' ', cbb); j--; }
+        else { put(ca, ' ', '-'); i--; }
+    }
+    if (reason == 1)
+        for (int64_t jj = j; jj > 0; jj--) put('-', ' ', b_chr[jj - 1]);
+    else if (reason == 2)
+        for (int64_t ii = i; ii > 0; ii--) put(a_chr[ii - 1], ' ', '-');
+    if (len > cap) return fail(GA_E_ARG, "output capacity too small");
+    std::reverse(oa, oa + len);
+    std::reverse(om, om + len);
+    std::reverse(ob, ob + len);
+    *out_len = len;
+    *tb_status = GA_TB_OK;
+    return GA_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* ga_last_error(void) { return g_err.c_str(); }
+
+int ga_device_count(int* count) {
+    if (!count) return fail(GA_E_ARG, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return fail(GA_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *count = n;
+    return GA_OK;
+}
+
+int ga_ctx_create(int device, ga_ctx** out) {
+    if (!out) return fail(GA_E_ARG, "null out");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(GA_E_ARG, "no such HIP device");
+    HIPCHK(hipSetDevice(device));
+    ga_ctx* c = new ga_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(GA_E_HIP, "hipStreamCreate failed");
+    }
+    for (auto& e : c->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete c;
+            return fail(GA_E_HIP, "hipEventCreate failed");
+        }
+    }
+    *out = c;
+    return GA_OK;
+}
+
+void ga_ctx_destroy(ga_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
+                      &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
+                      &c->result, &c->halo_in, &c->prog})
+        b->release();
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int ga_problem_set(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b, int64_t n, const ga_costs* cs,
+                   const int32_t* row0, const int32_t* col0) {
+    if (int r = check_ctx(c)) return r;
+    c->slab = false;
+    return load_problem(c, a, m, b, n, cs, row0, col0, 0, n);
+}
+
+int ga_problem_fill(ga_ctx* c, int32_t flags, int64_t* cost_out, int32_t* full_out) {
+    if (int r = check_ctx(c)) return r;
+    if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
+    if ((flags & GA_FILL_FULL) && !full_out) return fail(GA_E_ARG, "GA_FILL_FULL needs full_out");
+    if (int r = enqueue_fill(c, flags)) return r;
+    return finish_fill(c, cost_out, (flags & GA_FILL_FULL) ? full_out : nullptr);
+}
+
+int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
+                         char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
+    if (int r = check_ctx(c)) return r;
+    if (!c->filled_tb) return fail(GA_E_STATE, "traceback needs a GA_FILL_TRACEBACK fill first");
+    if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
+    std::vector<uint16_t> tab;
+    std::vector<PyMT> snaps;
+    build_rng(mt_state, c->m + c->n + 1, tab, snaps);
+    if (int r = run_walk(c, tab)) return r;
+    return finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+}
+
+int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
+                     char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    if (int r = check_ctx(c)) return r;
+    if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
+    if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
+    if (int r = enqueue_fill(c, GA_FILL_TRACEBACK)) return r;
+    // the tie-break table is built on the host while the device fills
+    std::vector<uint16_t> tab;
+    std::vector<PyMT> snaps;
+    build_rng(mt_state, c->m + c->n + 1, tab, snaps);
+    if (int r = run_walk(c, tab)) return r;
+    if (int r = finish_fill(c, cost_out, nullptr)) return r;
+    return finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+}
+
+// ---------------------------------------------------------------- slabs
+int ga_problem_set_slab(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b, int64_t n, const ga_costs* cs,
+                        int64_t col_begin, int64_t col_end) {
+    if (int r = check_ctx(c)) return r;
+    c->slab = true;
+    if (int r = load_problem(c, a, m, b, n, cs, nullptr, nullptr, col_begin, col_end)) return r;
+    HIPCHK(c->halo_in.ensure(sizeof(int2) * (m + 1)));
+    HIPCHK(c->prog.ensure(sizeof(unsigned) * 64));
+    HIPCHK(hipMemset(c->prog.p, 0, sizeof(unsigned) * 64));
+    return GA_OK;
+}
+
+int ga_slab_buffers(ga_ctx* c, void** halo_in, uint32_t** halo_in_prog, void** halo_out, uint32_t** halo_out_prog) {
+    if (int r = check_ctx(c)) return r;
+    if (!c->slab) return fail(GA_E_STATE, "not a slab context");
+    if (halo_in) *halo_in = c->halo_in.p;
+    if (halo_in_prog) *halo_in_prog = c->prog.as<uint32_t>();
+    if (halo_out) *halo_out = c->hand.as<int2>() + (size_t)(c->nslabs - 1) * (c->m + 1);
+    if (halo_out_prog) *halo_out_prog = c->prog.as<uint32_t>() + 1;
+    return GA_OK;
+}
+
+int ga_slab_fill_launch(ga_ctx* c, int32_t flags) {
+    if (int r = check_ctx(c)) return r;
+    if (!c->slab) return fail(GA_E_STATE, "not a slab context");
+    HIPCHK(hipMemsetAsync(c->prog.p, 0, sizeof(unsigned) * 2, c->stream));
+    return enqueue_fill(c, flags & GA_FILL_TRACEBACK);
+}
+
+int ga_slab_fill_finish(ga_ctx* c, int64_t* cost_out) {
+    if (int r = check_ctx(c)) return r;
+    return finish_fill(c, cost_out, nullptr);
+}
+
+int ga_stream_wait_ge(void* stream, uint32_t* prog, uint32_t value) {
+    HIPCHK(hipStreamWaitValue32((hipStream_t)stream, prog, value, hipStreamWaitValueGte, 0xffffffffu));
+    return GA_OK;
+}
+
+int ga_stream_write(void* stream, uint32_t* prog, uint32_t value) {
+    HIPCHK(hipStreamWriteValue32((hipStream_t)stream, prog, value, 0));
+    return GA_OK;
+}
+
+void* ga_ctx_stream(ga_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ga_last_kernel_ms(ga_ctx* c, float* fill_ms, float* walk_ms) {
+    if (!c) return fail(GA_E_ARG, "null context");
+    if (fill_ms) *fill_ms = c->fill_ms;
+    if (walk_ms) *walk_ms = c->walk_ms;
+    return GA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Optimal global alignment on MI355X -- drop-in for globalign's hot path.
+
+Public surface (mirrors iamgiddyaboutgit/globalign src/globalign/globaligner.py):
+
+  find_global_alignment(...) -> AlignmentResults        globaligner.py:132-314
+  make_dp_array / dp_array_forward / dp_array_backward   globaligner.py:756-821, 366-392, 395-593
+  main()  (the `globaligner` CLI)                        globaligner.py:23-129
+plus GlobalAligner, a reusable façade bound to one GPU that can lift the
+reference's m*n < 2e7 cap.
+
+The three DP functions run on the GPU through the C ABI in
+include/globalign_amd.h; there is no CPU fallback.  Tie-breaking consumes the
+process-global ``random`` state exactly like the reference (18
+``random.choice`` calls per traceback step), so with the same
+``random.seed`` the alignment strings are identical.
+"""
+import argparse
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+
+from . import _native
+from .results import AlignmentResults, final_cost_to_score
+from .scoring import MAX_SEQ_LEN_PROD, get_max_val, validate_and_transform_args
+
+__version__ = "0.1.0"
+
+
+def _mt_words():
+    st = random.getstate()
+    return np.array(st[1], dtype=np.uint32)
+
+
+def _set_mt_words(words):
+    random.setstate((3, tuple(int(x) for x in words), None))
+
+
+class GlobalAligner:
+    """Reusable aligner bound to one GPU.
+
+    ``GlobalAligner(**settings).align(seq_1, seq_2)`` accepts the same keyword
+    settings as find_global_alignment (scores, costs, matrix name/path, gap
+    options) and returns an AlignmentResults.  ``max_seq_len_prod=None``
+    lifts the reference's m*n < 2e7 API cap (the device path is sized for
+    100k x 100k and beyond); ``traceback=False`` returns the score only.
+    """
+
+    def __init__(self, scoring_mat_name=None, scoring_mat_path=None, match_score=None, mismatch_score=None,
+                 mismatch_cost=None, gap_open_score=None, gap_open_cost=None, gap_extension_score=None,
+                 gap_extension_cost=None, device=0, max_seq_len_prod=MAX_SEQ_LEN_PROD, traceback=True):
+        self.settings = dict(scoring_mat_name=scoring_mat_name, scoring_mat_path=scoring_mat_path,
+                             match_score=match_score, mismatch_score=mismatch_score, mismatch_cost=mismatch_cost,
+                             gap_open_score=gap_open_score, gap_open_cost=gap_open_cost,
+                             gap_extension_score=gap_extension_score, gap_extension_cost=gap_extension_cost)
+        self.device = device
+        self.max_seq_len_prod = max_seq_len_prod
+        self.traceback = traceback
+
+    def align(self, seq_1=None, seq_2=None, input_fasta=None, output=None):
+        good = validate_and_transform_args(input_fasta, output, seq_1, seq_2, max_seq_len_prod=self.max_seq_len_prod,
+                                           **self.settings)
+        return _align_validated(good, device=self.device, traceback=self.traceback)
+
+
+def _align_validated(good, device=0, traceback=True):
+    seq_1, seq_2, scoring_mat, costing_mat, gap_open_score, gap_open_cost, output = good
+    tables = _native.CostTables(costing_mat, gap_open_cost)
+    eng = _native.default_engine(device)
+    eng.load(tables.codes(seq_1), tables.codes(seq_2), tables)
+    if traceback:
+        cost, (a, mid, b), status, mt = eng.align(_mt_words(), seq_1, seq_2)
+        _set_mt_words(mt)  # the reference's random.choice calls advance the global state
+        if status == _native.GA_TB_INDEX_ERROR:
+            raise IndexError("string index out of range")  # reference behaviour for m==1 / n==1 walks (A.5)
+    else:
+        cost, _ = eng.fill(traceback=False)
+        a = mid = b = None
+    score = final_cost_to_score(cost=cost, m=len(seq_1), n=len(seq_2), max_score=get_max_val(scoring_mat))
+    return AlignmentResults(a, mid, b, cost, score, scoring_mat, costing_mat, gap_open_score, gap_open_cost, output)
+
+
+def find_global_alignment(input_fasta=None, output=None, seq_1=None, seq_2=None, scoring_mat_name=None,
+                          scoring_mat_path=None, match_score=None, mismatch_score=None, mismatch_cost=None,
+                          gap_open_score=None, gap_open_cost=None, gap_extension_score=None,
+                          gap_extension_cost=None) -> AlignmentResults:
+    """Optimal global alignment of seq_1 and seq_2 (Needleman-Wunsch / Gotoh affine gaps).
+
+    Same arguments, defaults, validation and result as globalign's
+    find_global_alignment; the DP fill and traceback run on the GPU."""
+    good = validate_and_transform_args(input_fasta, output, seq_1, seq_2, scoring_mat_name, scoring_mat_path,
+                                       match_score, mismatch_score, mismatch_cost, gap_open_score, gap_open_cost,
+                                       gap_extension_score, gap_extension_cost)
+    return _align_validated(good)
+
+
+# --------------------------------------------------------------------------------
+# The reference's DP building blocks, over its nested-list representation
+# (list of rows of (level0, level1, level2) tuples).  They are thin shims over
+# the same device kernels and exist so code written against globalign's
+# internals (e.g. its own test-suite) keeps working.
+
+def make_dp_array(seq_1, seq_2, costing_mat, max_cost, gap_open_cost):
+    """(m+1) x (n+1) list with row 0 / column 0 set and None inside (globaligner.py:756-821)."""
+    m, n = len(seq_1), len(seq_2)
+    dp = [[None] * (n + 1) for _ in range(m + 1)]
+    big = (max_cost + 1) * max(m, n)
+    dp[0][0] = (0, 0, 0)
+    if n >= 1:
+        x = gap_open_cost + costing_mat["-"][seq_2[0]]
+        dp[0][1] = (big, x, big)
+        for j in range(2, n + 1):
+            x += costing_mat["-"][seq_2[j - 1]]
+            dp[0][j] = (big, x, big)
+    else:
+        return dp
+    if m >= 1:
+        y = gap_open_cost + costing_mat[seq_1[0]]["-"]
+        dp[1][0] = (big, big, y)
+        for i in range(2, m + 1):
+            y += costing_mat[seq_1[i - 1]]["-"]
+            dp[i][0] = (big, big, y)
+    return dp
+
+
+def _boundary_arrays(dp_array, m, n):
+    row0 = np.array([dp_array[0][j] for j in range(n + 1)], dtype=np.int64).reshape(-1)
+    col0 = np.array([dp_array[i][0] for i in range(m + 1)], dtype=np.int64).reshape(-1)
+    if np.abs(np.concatenate([row0, col0])).max(initial=0) >= 2 ** 31:
+        raise OverflowError("boundary values exceed the int32 range of the device path")
+    return row0.astype(np.int32), col0.astype(np.int32)
+
+
+def dp_array_forward(dp_array, seq_1, seq_2, costing_mat, gap_open_cost):
+    """Fill dp_array[i][j] for i, j >= 1 in place from its row 0 / column 0 (globaligner.py:366-392)."""
+    m, n = len(seq_1), len(seq_2)
+    if m == 0 or n == 0:
+        return None
+    tables = _native.CostTables(costing_mat, gap_open_cost)
+    row0, col0 = _boundary_arrays(dp_array, m, n)
+    eng = _native.default_engine()
+    eng.load(tables.codes(seq_1), tables.codes(seq_2), tables, row0=row0, col0=col0)
+    _, full = eng.fill(full=True)
+    for i in range(1, m + 1):
+        row = dp_array[i]
+        fi = full[i]
+        for j in range(1, n + 1):
+            row[j] = (int(fi[j, 0]), int(fi[j, 1]), int(fi[j, 2]))
+    return None
+
+
+def dp_array_backward(dp_array, seq_1, seq_2, costing_mat, gap_open_cost):
+    """Traceback of a filled dp_array -> (seq_1_aligned, middle_part, seq_2_aligned, cost) (globaligner.py:395-593).
+
+    The walk needs per-cell rank information, so the fill is recomputed on the
+    device from dp_array's row 0 / column 0."""
+    m, n = len(seq_1), len(seq_2)
+    tables = _native.CostTables(costing_mat, gap_open_cost)
+    row0, col0 = _boundary_arrays(dp_array, m, n)
+    eng = _native.default_engine()
+    eng.load(tables.codes(seq_1), tables.codes(seq_2), tables, row0=row0, col0=col0)
+    cost, (a, mid, b), status, mt = eng.align(_mt_words(), seq_1, seq_2)
+    _set_mt_words(mt)
+    if status == _native.GA_TB_INDEX_ERROR:
+        raise IndexError("string index out of range")
+    return a, mid, b, cost
+
+
+def main(argv=None):
+    """The `globaligner` command line (globaligner.py:23-129)."""
+    parser = argparse.ArgumentParser(description="Perform optimal global alignment of two nucleotide or amino acid "
+                                                 "sequences.")
+    parser.add_argument("--version", action="version", version=__version__, help="Prints the version and exits.")
+    parser.add_argument("-i", "--input_fasta", required=False,
+                        help="FASTA file with the two sequences to align (only the first 2 records are used).")
+    parser.add_argument("-o", "--output", required=False,
+                        help="Output file for the alignment; stdout when omitted.")
+    parser.add_argument("--seq_1", required=False, help="First sequence to align.")
+    parser.add_argument("--seq_2", required=False, help="Second sequence to align.")
+    parser.add_argument("--scoring_mat_name", required=False, help="BLOSUM50 or BLOSUM62.")
+    parser.add_argument("--scoring_mat_path", required=False, help="Path to a custom scoring matrix file.")
+    parser.add_argument("--match_score", required=False, help="Score for a match (default 2).")
+    parser.add_argument("--mismatch_score", required=False, help="Score for a mismatch (default -3).")
+    parser.add_argument("--mismatch_cost", required=False, help="Cost for a mismatch (default 5).")
+    parser.add_argument("--gap_open_score", required=False, help="Score for opening a run of gaps (default -4).")
+    parser.add_argument("--gap_open_cost", required=False, help="Cost for opening a run of gaps (default 4).")
+    parser.add_argument("--gap_extension_score", required=False, help="Score per gap (default -2).")
+    parser.add_argument("--gap_extension_cost", required=False, help="Cost per gap (default 3).")
+    args = parser.parse_args(argv)
+    results = find_global_alignment(**vars(args))
+    results.write()
+    return None
+
+
+if __name__ == "__main__":
+    sys.exit(main())

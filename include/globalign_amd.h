@@ -1,0 +1,120 @@
+/*
+ * globalign_amd.h -- C ABI of the MI355X affine-gap global-alignment engine.
+ *
+ * The reference (iamgiddyaboutgit/globalign) is pure CPython with no FFI; each
+ * entry point below replaces the Python function(s) cited next to it
+ * (paths relative to the reference's src/globalign/).  The Python host layer
+ * (globalign_amd/_native.py) binds these with ctypes; INTEGRATION.md shows
+ * the binding a globalign maintainer would add.
+ *
+ * Conventions: every function returns 0 on success or a negative GA_E* code;
+ * ga_last_error() then describes the failure (thread-local).  Host buffers
+ * are caller-owned; device buffers are owned by the context.  A context is
+ * bound to one GPU and is not thread-safe (one per host thread).
+ */
+#ifndef GLOBALIGN_AMD_H
+#define GLOBALIGN_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GA_OK 0
+#define GA_E_ARG -1      /* invalid argument (maps to ValueError)          */
+#define GA_E_HIP -2      /* HIP runtime failure (maps to RuntimeError)     */
+#define GA_E_RANGE -3    /* int32 range / size limit exceeded               */
+#define GA_E_STATE -4    /* call order violated (e.g. traceback before fill) */
+#define GA_E_TIMEOUT -5  /* a device-side wait exceeded its spin bound      */
+
+/* Python-visible outcome of a traceback (dp_array_backward semantics). */
+#define GA_TB_OK 0
+#define GA_TB_INDEX_ERROR 1 /* the reference raises IndexError */
+
+typedef struct ga_ctx ga_ctx;
+
+/* Integer tables derived from the costing matrix (start.py:500-557).  Codes
+ * index the alphabet in any fixed order; the gap character has a code too. */
+typedef struct {
+    int32_t K;              /* alphabet size including the gap code           */
+    const int32_t* sub;     /* K*K: costing_mat[x][y]                         */
+    const int32_t* gap_h;   /* K:   costing_mat['-'][y] (globaligner.py:347) */
+    const int32_t* gap_v;   /* K:   costing_mat[x]['-'] (globaligner.py:357) */
+    int32_t gap_open;       /* gap_open_cost >= 0                             */
+    int32_t max_cost;       /* get_max_val(costing_mat) (start.py:488-497)   */
+} ga_costs;
+
+/* Last error message of this thread ("" if none). */
+const char* ga_last_error(void);
+
+/* Number of visible HIP devices. */
+int ga_device_count(int* count);
+
+/* Create / destroy a context on HIP device `device`. */
+int ga_ctx_create(int device, ga_ctx** out);
+void ga_ctx_destroy(ga_ctx* ctx);
+
+/* Load a problem: sequence codes (host), tables, optional custom boundaries.
+ * Replaces make_dp_array (globaligner.py:756-821): when row0/col0 are NULL the
+ * boundary is the reference's (finite sentinel big=(max_cost+1)*max(m,n));
+ * otherwise row0 = 3*(n+1) and col0 = 3*(m+1) triples (M, X, Y) as in the
+ * reference's own test (tests/globaligner_test.py:8-33).  Uploads to HBM. */
+int ga_problem_set(ga_ctx* ctx, const uint8_t* a, int64_t m, const uint8_t* b, int64_t n, const ga_costs* costs,
+                   const int32_t* row0, const int32_t* col0);
+
+#define GA_FILL_TRACEBACK 1 /* store per-cell traceback words (needed by ga_problem_traceback) */
+#define GA_FILL_FULL 2      /* also return every cell's (M, X, Y) (small problems only)       */
+
+/* Matrix fill (dp_array_forward, globaligner.py:366-392 with
+ * get_next_best_costs :317-363) on the loaded problem.  *cost_out receives
+ * min(dp[m][n]) (globaligner.py:425).  With GA_FILL_FULL, full_out receives
+ * 3*(m+1)*(n+1) int32 (row-major, boundary included). */
+int ga_problem_fill(ga_ctx* ctx, int32_t flags, int64_t* cost_out, int32_t* full_out);
+
+/* Traceback walk (dp_array_backward :395-593, cost_ranks_dispatcher
+ * :595-685, take_* :688-753) on the last GA_FILL_TRACEBACK fill.
+ * mt_state: 625 words = random.getstate()[1] in, the state after the
+ * reference's random.choice calls out.  a_chr/b_chr: the upper-cased
+ * sequences.  out_* need cap >= m+n+1 bytes; strings are not terminated.
+ * *tb_status receives GA_TB_OK or GA_TB_INDEX_ERROR. */
+int ga_problem_traceback(ga_ctx* ctx, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* out_a,
+                         char* out_mid, char* out_b, int64_t cap, int64_t* out_len, int32_t* tb_status);
+
+/* fill + traceback in one call, overlapping the host-side tie-break table
+ * with the device fill (the whole find_global_alignment hot path,
+ * globaligner.py:258-302). */
+int ga_problem_align(ga_ctx* ctx, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* out_a,
+                     char* out_mid, char* out_b, int64_t cap, int64_t* out_len, int32_t* tb_status,
+                     int64_t* cost_out);
+
+/* ---- multi-GPU column slabs ----------------------------------
+ * A context can own the column slab [col_begin, col_end) of a larger problem
+ * (global m, n and boundary).  Its left edge arrives in `halo_in`
+ * ((m+1) x int2 of (H', h1') in the shifted space of DESIGN.md) guarded by
+ * the progress word `halo_in_prog` (rows available); its right edge is
+ * produced into ga_slab_halo_out() with progress word ga_slab_halo_out_prog().
+ * Both words live in uncached device memory so a stream can wait on / write
+ * them (hipStreamWaitValue32 / hipStreamWriteValue32) around RCCL send/recv. */
+int ga_problem_set_slab(ga_ctx* ctx, const uint8_t* a, int64_t m, const uint8_t* b, int64_t n, const ga_costs* costs,
+                        int64_t col_begin, int64_t col_end);
+int ga_slab_buffers(ga_ctx* ctx, void** halo_in, uint32_t** halo_in_prog, void** halo_out, uint32_t** halo_out_prog);
+/* Launch the slab fill asynchronously on the context's compute stream. */
+int ga_slab_fill_launch(ga_ctx* ctx, int32_t flags);
+/* Wait for the slab fill; returns H'(m, col_end) un-shifted (only meaningful on the last slab). */
+int ga_slab_fill_finish(ga_ctx* ctx, int64_t* cost_out);
+/* Enqueue on `stream` (a hipStream_t): wait until *prog >= value / write value to *prog. */
+int ga_stream_wait_ge(void* stream, uint32_t* prog, uint32_t value);
+int ga_stream_write(void* stream, uint32_t* prog, uint32_t value);
+/* The context's compute stream (hipStream_t). */
+void* ga_ctx_stream(ga_ctx* ctx);
+
+/* ---- measurement --------------------------------------------------------- */
+/* Device time (ms, HIP events on the launch stream) of the last fill kernel
+ * and of the last traceback walk kernel. */
+int ga_last_kernel_ms(ga_ctx* ctx, float* fill_ms, float* walk_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
