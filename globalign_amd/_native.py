@@ -41,8 +41,28 @@ class EngineError(RuntimeError):
 EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_fill_launch",
-    "ga_slab_fill_finish", "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms",
+    "ga_slab_fill_finish", "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms", "ga_last_timings",
 ]
+
+
+def _preload_hip_runtime():
+    """Keep ONE HIP runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64.so and resolves it by path, while
+    this library links libamdhip64.so.7.  If ours were loaded first and torch
+    imported later, the process would hold two HIP runtimes.  So when torch is
+    installed, load torch's runtime first (without importing torch): our
+    library then binds to it by SONAME, and torch finds it already loaded."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        C.CDLL(cand, mode=C.RTLD_GLOBAL)
 
 
 def load_library():
@@ -51,6 +71,7 @@ def load_library():
     with _lib_lock:
         if _lib is not None:
             return _lib
+        _preload_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"{LIB_PATH} not found: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')")
@@ -77,6 +98,7 @@ def load_library():
         L.ga_ctx_stream.argtypes = [vp]
         L.ga_ctx_stream.restype = vp
         L.ga_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.ga_last_timings.argtypes = [vp, C.POINTER(C.c_float)]
         _lib = L
         return L
 
@@ -189,6 +211,12 @@ class Engine:
         cost = C.c_int64(0)
         strings, st, mt = self._tb_call(self._L.ga_problem_align, mt_words, a_chr, b_chr, (C.byref(cost),))
         return cost.value, strings, st, mt
+
+    def timings(self):
+        """{fill_ms, walk_ms, rng_ms (host tie-break table), call_ms} of the last call."""
+        out = (C.c_float * 4)()
+        _check(self._L.ga_last_timings(self._h, out))
+        return dict(fill_ms=out[0], walk_ms=out[1], rng_ms=out[2], call_ms=out[3])
 
     def kernel_ms(self):
         f, w = C.c_float(0), C.c_float(0)

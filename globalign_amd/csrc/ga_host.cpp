@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -103,14 +104,22 @@ struct PyMT {
 
 constexpr int SNAP = 1024;  // MT snapshots every SNAP dispatches
 
-// One dispatcher call = 18 draws of sizes [3,2,2,2,3,2,2,2,3] x {match, mismatch}.
-// Only draws 0-3 (match) and 9-12 (mismatch) can decide a move; pack them.
-inline uint16_t dispatch_bits(PyMT& g) {
+// One dispatcher call = 18 draws of sizes [3,2,2,2,3,2,2,2,3] x {match, mismatch}
+// (the dict literal of cost_ranks_dispatcher, globaligner.py:598-672).  Only
+// draws 0-3 (match) and 9-12 (mismatch) can decide a move.  The step's entry
+// maps each candidate set S (bit k = level k is a minimum) to the level taken:
+// 2 bits at 2(S-1), match in bits 0-13, mismatch in bits 14-27.
+inline uint32_t dispatch_entry(PyMT& g) {
     static const unsigned sizes[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
     unsigned r[18];
     for (int d = 0; d < 18; d++) r[d] = g.below(sizes[d]);
-    return (uint16_t)(r[0] | (r[1] << 2) | (r[2] << 3) | (r[3] << 4) | (r[9] << 5) | (r[10] << 7) | (r[11] << 8) |
-                      (r[12] << 9));
+    uint32_t e = 0;
+    for (int half = 0; half < 2; half++) {
+        const unsigned* q = r + 9 * half;
+        const unsigned lv[8] = {0, 0, 1, q[1], 2, 2 * q[2], 1 + q[3], q[0]};  // S = 1..7
+        for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * (S - 1) + 14 * half);
+    }
+    return e;
 }
 
 }  // namespace
@@ -133,7 +142,11 @@ struct ga_ctx {
         ops, result;
     DevBuf halo_in{nullptr, 0, true}, prog{nullptr, 0, true};
     bool slab = false;
-    float fill_ms = 0.f, walk_ms = 0.f;
+    float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
+    bool dbg_on = false;
+    int ablation = -1;  // diagnostics: fill kernel ablation variant (-1 = product kernel)
+    int walk_waits = 0, walk_tiles = 0;
+    DevBuf dbg;
 };
 
 namespace {
@@ -212,8 +225,16 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
         HIPCHK(hipMemcpyAsync(c->bnd_row.p, row0, sizeof(int) * 3 * (n_all + 1), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(c->bnd_col.p, col0, sizeof(int) * 3 * (m + 1), hipMemcpyHostToDevice, c->stream));
     }
-    const long long stride = m + 2 * ga::QPAD;
-    HIPCHK(c->qp.ensure((size_t)stride * K * c->qbytes));
+    {
+        // sub' = sub - gV - gH, read by the fill's IO wave into its LDS query profile
+        std::vector<int> subp((size_t)K * K);
+        for (int x = 0; x < K; x++)
+            for (int y = 0; y < K; y++) subp[x * K + y] = cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y];
+        HIPCHK(c->qp.ensure(sizeof(int) * K * K));
+        HIPCHK(hipMemcpy(c->qp.p, subp.data(), sizeof(int) * K * K, hipMemcpyHostToDevice));
+        if (ga::fill_lds_bytes(c->CB, c->qbytes, true, K) > 160 * 1024)
+            return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
+    }
     HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
     HIPCHK(c->GHp.ensure(sizeof(int) * (n_all + 1)));
     HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
@@ -222,9 +243,9 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
     HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     HIPCHK(c->out_last.ensure(sizeof(int) * 4));
-    HIPCHK(c->result.ensure(sizeof(int) * 4));
+    HIPCHK(c->result.ensure(sizeof(int) * 8));
     HIPCHK(c->ops.ensure(m + n_all + 8));
-    HIPCHK(c->rng.ensure(sizeof(uint16_t) * (m + n_all + 2)));
+    HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->loaded = true;
     c->filled_tb = false;
@@ -247,14 +268,13 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     unsigned* fl = c->flags.as<unsigned>();
     // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
-    ga::launch_qp(c->stream, c->a.as<uint8_t>(), (int)m, c->sub.as<int>(), c->gh.as<int>(), c->gv.as<int>(), c->K,
-                  c->qp.p, m + 2 * ga::QPAD, c->qbytes);
     ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
                         c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
                         c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom);
     ga::FillArgs p{};
-    p.qp = c->qp.p;
-    p.qp_stride = m + 2 * ga::QPAD;
+    p.a = c->a.as<uint8_t>();
+    p.subp = c->qp.as<int>();
+    p.K = c->K;
     p.b = c->b.as<uint8_t>() + c->col0;
     p.top = c->top.as<int2>() + c->col0;
     if (c->slab && c->col0 > 0) {
@@ -280,8 +300,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     p.TC = c->TC;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
+    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 4 * c->nstripes));
+    p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    if (c->ablation >= 0 && c->CB == 1 && c->qbytes == 1 && !full) ga::launch_fill_ablation(c->stream, p, tb, c->ablation);
+    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     c->filled_tb = tb;
@@ -330,7 +353,11 @@ int finish_fill(ga_ctx* c, int64_t* cost_out, int32_t* full_out) {
 }
 
 // Tie-break table for up to `steps` dispatches + MT snapshots every SNAP.
-void build_rng(const uint32_t* state, int64_t steps, std::vector<uint16_t>& tab, std::vector<PyMT>& snaps) {
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void build_rng(const uint32_t* state, int64_t steps, std::vector<uint32_t>& tab, std::vector<PyMT>& snaps) {
     PyMT g;
     std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
     g.mti = (int)state[MTN];
@@ -339,20 +366,20 @@ void build_rng(const uint32_t* state, int64_t steps, std::vector<uint16_t>& tab,
     snaps.reserve(steps / SNAP + 1);
     for (int64_t k = 0; k < steps; k++) {
         if (k % SNAP == 0) snaps.push_back(g);
-        tab[k] = dispatch_bits(g);
+        tab[k] = dispatch_entry(g);
     }
     if (steps % SNAP == 0) snaps.push_back(g);
 }
 
 void state_after(const std::vector<PyMT>& snaps, int64_t D, uint32_t* out) {
     PyMT g = snaps[D / SNAP];
-    for (int64_t k = 0; k < D % SNAP; k++) (void)dispatch_bits(g);
+    for (int64_t k = 0; k < D % SNAP; k++) (void)dispatch_entry(g);
     std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
     out[MTN] = (uint32_t)g.mti;
 }
 
-int run_walk(ga_ctx* c, const std::vector<uint16_t>& tab) {
-    HIPCHK(hipMemcpyAsync(c->rng.p, tab.data(), sizeof(uint16_t) * tab.size(), hipMemcpyHostToDevice, c->stream));
+int run_walk(ga_ctx* c, const std::vector<uint32_t>& tab) {
+    HIPCHK(hipMemcpyAsync(c->rng.p, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice, c->stream));
     ga::WalkArgs w{};
     w.tb = c->tb.as<uint8_t>();
     w.CB = c->CB;
@@ -361,7 +388,7 @@ int run_walk(ga_ctx* c, const std::vector<uint16_t>& tab) {
     w.b = c->b.as<uint8_t>();
     w.bnd_row = c->bnd_row.as<int>();
     w.bnd_col = c->bnd_col.as<int>();
-    w.rng = c->rng.as<uint16_t>();
+    w.rng = c->rng.as<uint32_t>();
     w.nrng = (long long)tab.size();
     w.m = (int)c->m;
     w.n = (int)c->n;
@@ -379,8 +406,10 @@ inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 
 int finish_walk(ga_ctx* c, const std::vector<PyMT>& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
                 char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
-    int res[4];
-    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    int res[8];
+    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 8, hipMemcpyDeviceToHost, c->stream));
+    c->walk_waits = res[4];
+    c->walk_tiles = res[5];
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(&c->walk_ms, c->ev[2], c->ev[3]));
     const int64_t D = res[0];
@@ -490,7 +519,7 @@ int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const
     if (int r = check_ctx(c)) return r;
     if (!c->filled_tb) return fail(GA_E_STATE, "traceback needs a GA_FILL_TRACEBACK fill first");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
-    std::vector<uint16_t> tab;
+    std::vector<uint32_t> tab;
     std::vector<PyMT> snaps;
     build_rng(mt_state, c->m + c->n + 1, tab, snaps);
     if (int r = run_walk(c, tab)) return r;
@@ -502,14 +531,19 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     if (int r = check_ctx(c)) return r;
     if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
+    const double t0 = now_ms();
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK)) return r;
     // the tie-break table is built on the host while the device fills
-    std::vector<uint16_t> tab;
+    std::vector<uint32_t> tab;
     std::vector<PyMT> snaps;
+    const double t1 = now_ms();
     build_rng(mt_state, c->m + c->n + 1, tab, snaps);
+    c->rng_ms = (float)(now_ms() - t1);
     if (int r = run_walk(c, tab)) return r;
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
-    return finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+    const int rc = finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+    c->call_ms = (float)(now_ms() - t0);
+    return rc;
 }
 
 // ---------------------------------------------------------------- slabs
@@ -562,6 +596,39 @@ int ga_last_kernel_ms(ga_ctx* c, float* fill_ms, float* walk_ms) {
     if (!c) return fail(GA_E_ARG, "null context");
     if (fill_ms) *fill_ms = c->fill_ms;
     if (walk_ms) *walk_ms = c->walk_ms;
+    return GA_OK;
+}
+
+// Diagnostics (not in the public header): per-stripe s_memrealtime stamps of the next fills.
+int ga_debug_stamps(ga_ctx* c, int enable, unsigned long long* out, int64_t cap) {
+    if (!c) return fail(GA_E_ARG, "null context");
+    c->dbg_on = enable != 0;
+    if (out && c->dbg.p) {
+        const int64_t nb = std::min<int64_t>(cap, 4 * (int64_t)c->nstripes);
+        HIPCHK(hipMemcpy(out, c->dbg.p, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost));
+    }
+    return GA_OK;
+}
+
+int ga_debug_ablation(ga_ctx* c, int abl) {
+    if (!c) return fail(GA_E_ARG, "null context");
+    c->ablation = abl;
+    return GA_OK;
+}
+
+int ga_debug_walk(ga_ctx* c, int* out2) {
+    if (!c || !out2) return fail(GA_E_ARG, "null argument");
+    out2[0] = c->walk_waits;
+    out2[1] = c->walk_tiles;
+    return GA_OK;
+}
+
+int ga_last_timings(ga_ctx* c, float* out4) {
+    if (!c || !out4) return fail(GA_E_ARG, "null argument");
+    out4[0] = c->fill_ms;
+    out4[1] = c->walk_ms;
+    out4[2] = c->rng_ms;
+    out4[3] = c->call_ms;
     return GA_OK;
 }
 

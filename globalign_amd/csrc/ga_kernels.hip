@@ -60,27 +60,16 @@ __device__ __forceinline__ bool spin_ok(unsigned& spins, unsigned limit, unsigne
     return true;
 }
 
-// ----------------------------------------------------------------------------------
-// Query profile: qp[c][QPAD + i] = sub(a_i, c) - gV(a_i) - gH(c)  (i in [0,m)).
-// A lane owning column code c reads its row's sub' with one byte/short load whose
-// address is (uniform step) + (lane constant): no VALU work for the lookup.
-template <typename QT>
-__global__ void qp_kernel(const uint8_t* __restrict__ a, int m, const int* __restrict__ sub,
-                          const int* __restrict__ gh, const int* __restrict__ gv, int K, QT* __restrict__ qp,
-                          long long stride) {
-    long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    long long total = stride * K;
-    for (; idx < total; idx += (long long)gridDim.x * blockDim.x) {
-        int c = (int)(idx / stride);
-        long long p = idx - (long long)c * stride;
-        long long i = p - QPAD;
-        QT v = 0;
-        if (i >= 0 && i < m) {
-            int x = a[i];
-            v = (QT)(sub[x * K + c] - gv[x] - gh[c]);
-        }
-        qp[idx] = v;
+// Bounded spin for compute waves: LDS-only (no global memory op may appear in their
+// loop, or the compiler's vmcnt bookkeeping turns the prefetch waits into vmcnt(0)).
+__device__ __forceinline__ bool spin_ok_lds(unsigned& spins, unsigned limit, unsigned* abort_sh) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins >= limit) {
+        __hip_atomic_store(abort_sh, 1u, __ATOMIC_RELAXED, WGS);
+        return false;
     }
+    if ((spins & 255u) == 0 && __hip_atomic_load(abort_sh, __ATOMIC_RELAXED, WGS)) return false;
+    return true;
 }
 
 // ----------------------------------------------------------------------------------
@@ -185,13 +174,32 @@ struct StepState {
     int Xout;  // this lane's h1' of the current row  (to lane l+1)
 };
 
-template <int CB, bool MASK, bool FULL>
+// BYTES of query profile (one chunk's sub' values for one lane), as raw dwords.
+template <int BYTES>
+struct QPack {
+    static constexpr int NWD = (BYTES + 3) / 4;
+    uint32_t w[NWD];
+    template <typename T>
+    __device__ static QPack load(const T* p) {
+        QPack r;
+        __builtin_memcpy(r.w, p, sizeof(r.w));
+        return r;
+    }
+    template <typename QT>
+    __device__ __forceinline__ int get(int u) const {
+        if (sizeof(QT) == 1) return (int)(int8_t)(w[u >> 2] >> (8 * (u & 3)));
+        return (int)(int16_t)(w[u >> 1] >> (16 * (u & 1)));
+    }
+};
+
+// ABL: diagnostic ablations (0 in the product): 2 = no DPP (timing only)
+template <int CB, bool MASK, bool FULL, int ABL = 0>
 __device__ __forceinline__ void dp_step(StepState& s, int2 lin, int sub, int o, unsigned op1, int t, int lane, int m,
                                         bool colok, uint32_t& accw, int sh, int* full, int fullW, int jcol) {
     constexpr int W = TbFmt<CB>::W;
     // left neighbour (lane l-1, previous step); lane 0 takes the slab edge from the ring
-    const int HL = __builtin_amdgcn_update_dpp(lin.x, s.Hout, 0x138, 0xf, 0xf, false);  // wave_shr:1
-    const int XL = __builtin_amdgcn_update_dpp(lin.y, s.Xout, 0x138, 0xf, 0xf, false);
+    const int HL = (ABL & 2) ? (lin.x ^ s.Hout) : __builtin_amdgcn_update_dpp(lin.x, s.Hout, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const int XL = (ABL & 2) ? (lin.y ^ s.Xout) : __builtin_amdgcn_update_dpp(lin.y, s.Xout, 0x138, 0xf, 0xf, false);
     const int Hd = s.HLp;
     s.HLp = HL;
     bool act = true;
@@ -222,37 +230,83 @@ __device__ __forceinline__ void dp_step(StepState& s, int2 lin, int sub, int o, 
 
 
 
-template <int CB, typename QT, bool TB, bool FULL>
-__global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
+// ABL (diagnostic ablations, 0 in the product): 1 = no ring write, 2 = no DPP, 4 = no ring
+// read, 8 = no query-profile reads, 16 = no inter-wave waits.
+//
+// Workgroup = NW compute waves + 2 IO waves, all communication through LDS.
+// Compute waves issue no HBM operation at all (their steady loop is VALU + LDS):
+//   * IO-A (wave NW) moves the slab's left edge in (HBM -> ring 0), the right edge
+//     out (ring NW -> HBM, write-through + progress word) and fills the query
+//     profile ring qring[code][row] from seq_1 (sub' = sub - gV - gH);
+//   * IO-B (wave NW+1) streams the compute waves' traceback words from LDS
+//     staging slots to HBM.
+// LDS layout (dynamic, byte offsets from FillLds::*).
+struct FillLds {
+    static constexpr int CNT = 0;                                  // u32 counters (see CI_*)
+    static constexpr int RINGS = 256;                              // (NW+1) x RING x int2
+    static constexpr int DUMMY = RINGS + (NW + 1) * RING * 8;      // 64 x 17 x int2 sink for lanes 0..62
+    static constexpr int TBST = DUMMY + 64 * 17 * 8;               // NW x TBS x 64 x 16 B
+    static constexpr int QRING_TB = TBST + NW * TBS * 1024;
+    static constexpr int QRING_NOTB = TBST;
+};
+enum { CI_PROD = 0, CI_CONS = 8, CI_TBPROD = 16, CI_TBCONS = 24, CI_ABORT = 32, CI_SLAB = 33 };
+
+template <int CB, typename QT, bool TB, bool FULL, int ABL = 0>
+__global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
     constexpr int SPC = TbFmt<CB>::SPC;
-    __shared__ int2 ring[NW + 1][RING];
-    __shared__ unsigned prod[NW + 1], cons[NW + 1];
-    __shared__ int slab_sh;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    unsigned* cnt = reinterpret_cast<unsigned*>(smem + FillLds::CNT);
+    int2* rings = reinterpret_cast<int2*>(smem + FillLds::RINGS);
+    int2* dummy = reinterpret_cast<int2*>(smem + FillLds::DUMMY);
+    uint4* tbst = reinterpret_cast<uint4*>(smem + FillLds::TBST);
+    QT* qring = reinterpret_cast<QT*>(smem + (TB ? FillLds::QRING_TB : FillLds::QRING_NOTB));
+    unsigned* prod = cnt + CI_PROD;
+    unsigned* cons = cnt + CI_CONS;
+    unsigned* tbprod = cnt + CI_TBPROD;
+    unsigned* tbcons = cnt + CI_TBCONS;
+    unsigned* abort_sh = cnt + CI_ABORT;
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) slab_sh = (int)atomicAdd(p.ticket, 1u);
-    if (threadIdx.x <= NW) { prod[threadIdx.x] = 0; cons[threadIdx.x] = 0; }
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave index: uniform
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
     __syncthreads();
-    const int g = slab_sh;
+    if (threadIdx.x == 0) cnt[CI_SLAB] = atomicAdd(p.ticket, 1u);
+    __syncthreads();
+    const int g = __builtin_amdgcn_readfirstlane((int)cnt[CI_SLAB]);  // uniform: scalar branches below
     const unsigned m = (unsigned)p.m;
+    const int QSTRIDE = QROWS + SPC;  // per code: QROWS slots + SPC mirrored rows (no wrap inside a chunk)
+    const int T = (int)m + 63;
+    const int nchunks = (T + SPC - 1) / SPC;
 
     if (w == NW) {
-        // ---------------- IO wave: slab edges HBM <-> LDS rings ----------------
+        // ---------------- IO-A: slab edges HBM <-> LDS rings, query profile ----------------
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
         const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
         const bool src_sc1 = g != 0 || p.left_prog != nullptr;
         int2* dst = p.hand + (long long)g * (m + 1);
+        const int K = p.K;
         unsigned in_next = 0, out_next = 0, spins = 0;
         while (in_next < m || out_next < m) {
             bool moved = false;
             if (in_next < m) {
-                const unsigned space = lds_ld(&cons[0]) + RING;
+                // ring 0 slots are reused after wave 0 read them; query-profile rows after
+                // the last compute wave's lanes all passed them (its output count)
+                const unsigned space = min(lds_ld(&cons[0]) + RING, lds_ld(&prod[NW]) + QROWS - 2 * SPC);
                 const unsigned avail = src_prog ? min(g_ld(src_prog), m) : m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
                     const unsigned r = in_next + 1 + lane;
-                    if (r <= hi) ring[0][r & RMASK] = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
+                    if (r <= hi) {
+                        rings[(r + 62) & RMASK] = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
+                        const int x = p.a[r - 1];
+                        const int slot = r & QMASK;
+                        const int* sp = p.subp + x * K;
+                        for (int c = 0; c < K; c++) {
+                            const QT v = (QT)sp[c];
+                            qring[c * QSTRIDE + slot] = v;
+                            if (slot < SPC) qring[c * QSTRIDE + QROWS + slot] = v;
+                        }
+                    }
                     if (lane == 0) lds_st(&prod[0], hi);
                     in_next = hi;
                     moved = true;
@@ -263,7 +317,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
                 const unsigned hi = min(avail, out_next + 64);
                 if (hi > out_next && (hi - out_next >= GOUT || hi == m)) {
                     const unsigned r = out_next + 1 + lane;
-                    if (r <= hi) g_st64(dst + r, ring[NW][r & RMASK]);
+                    if (r <= hi) g_st64(dst + r, rings[NW * RING + ((r + 62) & RMASK)]);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) {
                         g_st(p.hand_prog + g, hi);
@@ -276,7 +330,56 @@ __global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
                 }
             }
             if (!moved) {
-                if (!spin_ok(spins, limit, p.abort_word)) break;
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) {  // a compute wave gave up
+                    g_st(p.abort_word, 1u);
+                    break;
+                }
+                if (!spin_ok(spins, limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
+            } else {
+                spins = 0;
+            }
+        }
+        return;
+    }
+
+    if (w == NW + 1) {
+        // ---------------- IO-B: traceback words LDS staging -> HBM ----------------
+        if (!TB) return;
+        unsigned done[NW];
+        int nlive = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++) {
+            done[k] = 0;
+            nlive += (g * NW + k) < p.nstripes;
+        }
+        unsigned spins = 0;
+        for (;;) {
+            bool moved = false, all = true;
+#pragma unroll
+            for (int k = 0; k < NW; k++) {
+                if (k >= nlive) continue;
+                const unsigned avail = lds_ld(&tbprod[k]);
+                if (avail > done[k]) {
+                    const long long s = (long long)g * NW + k;
+                    uint4* dstp = reinterpret_cast<uint4*>(p.tb) + (s * p.TC) * 64 + lane;
+                    for (unsigned cc = done[k]; cc < avail; cc++)
+                        dstp[(long long)cc * 64] = tbst[(k * TBS + (cc % TBS)) * 64 + lane];
+                    done[k] = avail;
+                    if (lane == 0) lds_st(&tbcons[k], avail);  // the LDS reads above are complete
+                    moved = true;
+                }
+                all &= done[k] >= (unsigned)nchunks;
+            }
+            if (all) break;
+            if (!moved) {
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) break;
+                if (!spin_ok(spins, p.spin_limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
             } else {
                 spins = 0;
             }
@@ -291,7 +394,7 @@ __global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
     const bool colok = live && jcol <= p.n;
     const bool full_stripe = live && (s * 64 + 64 <= p.n);
     const int bcode = colok ? p.b[jcol - 1] : 0;
-    const QT* qpl = reinterpret_cast<const QT*>(p.qp) + (long long)bcode * p.qp_stride + QPAD - lane;
+    const QT* qcol = qring + bcode * QSTRIDE;
     StepState st;
     {
         const int jt = colok ? jcol : 0;
@@ -302,63 +405,80 @@ __global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
     }
     const int o = p.o;
     const unsigned op1 = (unsigned)o + 1u;
-    const int T = (int)m + 63;
-    const int nchunks = (T + SPC - 1) / SPC;
-    int2* rin = ring[w];
-    int2* rout = ring[w + 1];
-    unsigned spins = 0;
-    int q[SPC], qn[SPC];
-#pragma unroll
-    for (int u = 0; u < SPC; u++) q[u] = qpl[u];
-    uint8_t* tbl = TB ? p.tb + ((long long)s * p.TC * 64 + lane) * 16 : nullptr;
+    const int2* rin = rings + w * RING;
+    // lanes 0..62 write into their own sink rows, 17 int2 apart: the per-lane stride of 34
+    // dwords spreads a 16-lane ds_write_b64 group over all 32 banks (no conflicts)
+    int2* const aout = lane == 63 ? rings + (w + 1) * RING : dummy + lane * 17;
+    const unsigned aout_mask = lane == 63 ? (unsigned)RMASK : 0u;
+    unsigned spins = 0, avail = 0, outfree = RING, tbfree = TBS;
+    unsigned long long stamp0 = 0, stamp1 = 0;
     bool ok = true;
 
     for (int c = 0; c < nchunks && ok; c++) {
         const int t0 = c * SPC;
-        // inputs: rows t0+1 .. t0+SPC must be in the ring
+        if (p.dbg != nullptr && c == 1) stamp0 = __builtin_amdgcn_s_memrealtime();
+        if (p.dbg != nullptr && c == nchunks / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
+        // inputs: rows t0+1 .. t0+SPC in ring w (counter read only when needed)
         const unsigned need = min((unsigned)(t0 + SPC), m);
-        while (lds_ld(&prod[w]) < need) {
-            if (!spin_ok(spins, p.spin_limit, p.abort_word)) { ok = false; break; }
+        while (!(ABL & 16) && avail < need) {
+            avail = lds_ld(&prod[w]);
+            if (avail >= need) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
         }
-        // outputs: rows t0-62 .. t0+SPC-63 will be written; keep RING rows of slack
+        // outputs: rows t0-62 .. t0+SPC-63; a ring slot is reused RING rows later
         const int hi_out = t0 + SPC - 63;
-        if (hi_out - RING > 0) {
-            while ((int)lds_ld(&cons[w + 1]) < hi_out - RING) {
-                if (!spin_ok(spins, p.spin_limit, p.abort_word)) { ok = false; break; }
-            }
+        while (!(ABL & 16) && (int)outfree < hi_out) {
+            outfree = lds_ld(&cons[w + 1]) + RING;
+            if ((int)outfree >= hi_out) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
+        }
+        // traceback staging slot c % TBS must have been drained (chunk c - TBS)
+        while (TB && live && !(ABL & 16) && tbfree < (unsigned)c + 1u) {
+            tbfree = lds_ld(&tbcons[w]) + TBS;
+            if (tbfree >= (unsigned)c + 1u) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
         }
         if (!ok) break;
         spins = 0;
-        if (lane == 0) lds_st(&cons[w], min((unsigned)t0, m));
-        // prefetch next chunk's substitution values
+        if (lane == 0) __hip_atomic_store(&cons[w], min((unsigned)t0, m), RLX, WGS);
+        // this chunk's left-edge rows (broadcast) and substitution values (per lane)
+        int2 lin[SPC];
+        int qv[SPC];
+        const QT* qa = qcol + ((t0 + 1 - lane) & QMASK);
 #pragma unroll
-        for (int u = 0; u < SPC; u++) qn[u] = qpl[t0 + SPC + u];
+        for (int u = 0; u < SPC; u++) {
+            lin[u] = (ABL & 4) ? make_int2(t0 + u, u) : rin[(t0 + 63 + u) & RMASK];
+            qv[u] = (ABL & 8) ? (u - 3) : (int)qa[u];
+        }
+        int2* ao = aout + ((unsigned)t0 & aout_mask);
         uint32_t acc[4] = {0, 0, 0, 0};
         const bool steady = full_stripe && t0 >= 63 && t0 + SPC - 1 <= (int)m - 1;
         if (steady) {
 #pragma unroll
             for (int u = 0; u < SPC; u++) {
-                const int t = t0 + u;
-                const int2 lin = rin[(t + 1) & RMASK];
-                dp_step<CB, false, FULL>(st, lin, q[u], o, op1, t, lane, m, true, acc[(u * CB) >> 2],
-                                         (u * CB * 8) & 31, p.full, p.n + 1, jcol);
-                if (lane == 63) rout[(t - 62) & RMASK] = make_int2(st.Hout, st.Xout);
+                dp_step<CB, false, FULL, ABL>(st, lin[u], qv[u], o, op1, t0 + u, lane, m, true, acc[(u * CB) >> 2],
+                                              (u * CB * 8) & 31, p.full, p.n + 1, jcol);
+                if (!(ABL & 1)) ao[u] = make_int2(st.Hout, st.Xout);
             }
         } else {
 #pragma unroll
             for (int u = 0; u < SPC; u++) {
-                const int t = t0 + u;
-                const int2 lin = rin[(t + 1) & RMASK];
-                dp_step<CB, true, FULL>(st, lin, q[u], o, op1, t, lane, m, colok, acc[(u * CB) >> 2],
-                                        (u * CB * 8) & 31, p.full, p.n + 1, jcol);
-                const int r = t - 62;
-                if (r >= 1 && r <= (int)m && lane == 63) rout[r & RMASK] = make_int2(st.Hout, st.Xout);
+                dp_step<CB, true, FULL, ABL>(st, lin[u], qv[u], o, op1, t0 + u, lane, m, colok, acc[(u * CB) >> 2],
+                                             (u * CB * 8) & 31, p.full, p.n + 1, jcol);
+                if (!(ABL & 1)) ao[u] = make_int2(st.Hout, st.Xout);
             }
         }
-        if (TB && live) *reinterpret_cast<uint4*>(tbl + (long long)c * 1024) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-        if (hi_out >= 1 && lane == 0) lds_st(&prod[w + 1], min((unsigned)hi_out, m));
-#pragma unroll
-        for (int u = 0; u < SPC; u++) q[u] = qn[u];
+        if (TB && live) tbst[(w * TBS + (c % TBS)) * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+        if (lane == 0) {
+            // one release (lgkmcnt(0)) covers the ring rows and the staged words
+            if (TB && live) lds_st(&tbprod[w], (unsigned)c + 1u);
+            if (hi_out >= 1) lds_st(&prod[w + 1], min((unsigned)hi_out, m));
+        }
+    }
+    if (p.dbg != nullptr && lane == 0 && live) {
+        p.dbg[4 * s] = stamp0;
+        p.dbg[4 * s + 1] = stamp1;
+        p.dbg[4 * s + 2] = __builtin_amdgcn_s_memrealtime();
     }
     // the lane owning column n writes the final H' (cost = H' + phi(m, n))
     if (ok && colok && jcol == p.n) p.out_last[0] = st.Hout;
@@ -367,12 +487,18 @@ __global__ void __launch_bounds__(64 * (NW + 1)) fill_kernel(FillArgs p) {
 // ----------------------------------------------------------------------------------
 // Traceback walk (dp_array_backward, globaligner.py:395-593).
 //
-// One workgroup.  A WR x WC window of decoded rank sets (S0|S1<<3|S2<<6 per cell)
-// is staged in LDS around the walker; thread 0 walks, every thread restages the
-// window when the walk leaves it.  Degenerate inputs (the walk
-// visits row 0 / column 0 and wraps with Python negative indexing) are
-// reproduced cell by cell from HBM.
-
+// One workgroup of four waves.  Wave 0 walks; waves 1-3 keep a 3x3
+// direct-mapped cache of decoded 64x64 tiles (tile = 64 rows x one 64-column
+// stripe) filled ahead of the walker: the path is monotone (up/left), so the
+// tiles it can reach next are the 3x3 block above-left of its current tile,
+// and slot (ti mod 3, tj mod 3) gives every tile of that block its own slot.
+// A cached cell is a u16: rank sets S0|S1<<3|S2<<6 (see sets_from_code) and
+// bit 9 = (a_i == b_j).  The per-step tie-break choice comes from a host table
+// (two 7x2-bit maps from candidate set S to level, bits 2(S-1), for match and
+// mismatch), so a
+// step is: one LDS read, a shift and a mask.  Degenerate inputs (SURVEY A.5:
+// the walk visits row 0 / column 0 and wraps with Python negative indexing)
+// are reproduced cell by cell from HBM.
 
 __device__ __forceinline__ int argmin3(long long x, long long y, long long z) {
     long long h = x < y ? x : y;
@@ -405,114 +531,160 @@ __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, i
     return v;
 }
 
-// choose a level from the candidate set using the step's tie-break bits
-// (dispatcher entries :599-671: 3-way (0,0,0)-type uses draw 0/9, pairs use 1-3/10-12)
-__device__ __forceinline__ int choose(int S, unsigned bits) {
-    switch (S) {
-        case 1: return 0;
-        case 2: return 1;
-        case 4: return 2;
-        case 7: return (int)(bits & 3u);
-        case 3: return (int)((bits >> 2) & 1u);          // (match, gap1)
-        case 5: return 2 * (int)((bits >> 3) & 1u);      // (match, gap2)
-        default: return 1 + (int)((bits >> 4) & 1u);    // 6: (gap1, gap2)
+constexpr int TT = 64;  // tile edge
+
+__device__ __forceinline__ int slot_of(int ti, int tj) { return (ti % 3) * 3 + (tj % 3); }
+
+// One loader wave decodes tile (ti, tj) into `dst`: lane = column; each lane
+// walks the 16-byte chunks of its column's traceback stream that cover the
+// tile's 64 rows.
+template <int CB>
+__device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* dst, uint8_t* sa, int lane) {
+    constexpr int SPC = 16 / CB;
+    constexpr int KMAX = TT / SPC + 1;
+    const int i0 = ti * TT + 1;                       // first row of the tile
+    const int j = tj * TT + lane + 1;                 // this lane's column
+    sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
+    const bool colok = j <= w.n;
+    const int bj = colok ? w.b[j - 1] : 0xfe;
+    const int tfirst = i0 - 1 + lane;                 // t of row i0 in this column
+    const int q0 = tfirst / SPC;
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC) * 64 + lane;
+    uint4 ch[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+        const int q = q0 + k;
+        ch[k] = (colok && q < w.TC) ? base[(long long)q * 64] : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+        const unsigned wd[4] = {ch[k].x, ch[k].y, ch[k].z, ch[k].w};
+#pragma unroll
+        for (int u = 0; u < SPC; u++) {
+            const int r = (q0 + k) * SPC + u - tfirst;   // tile row
+            if (r >= 0 && r < TT) {
+                unsigned code = wd[(u * CB) >> 2] >> ((u * CB * 8) & 31);
+                if (CB == 1) code &= 0xffu;
+                else if (CB == 2) code &= 0xffffu;
+                const int v = sets_from_code(code, CB, w.o) | ((int)(sa[r] == bj) << 9);
+                dst[r * TT + lane] = (uint16_t)v;
+            }
+        }
     }
 }
 
+template <int CB>
 __global__ void __launch_bounds__(256) walk_kernel(WalkArgs w) {
-    __shared__ uint16_t win[WR * WC];
-    __shared__ uint8_t wa[WR], wb[WC];
-    __shared__ uint16_t wr[RW];
-    __shared__ int st[8];  // i, j, L, D, h, first, done, reason
-    const int tid = threadIdx.x;
-    const int m = w.m, n = w.n, o = w.o;
-    if (tid == 0) {
-        st[0] = m; st[1] = n; st[2] = 0; st[3] = 0; st[4] = 0; st[5] = 1; st[6] = 0; st[7] = 0;
-    }
+    __shared__ uint16_t tiles[9][TT * TT];
+    __shared__ uint8_t sa[3][TT];
+    __shared__ int tag[9];
+    __shared__ int cur_tile;
+    __shared__ int walk_done;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < 9) tag[threadIdx.x] = -1;
+    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; }
     __syncthreads();
+    const int m = w.m, n = w.n, o = w.o;
+
+    if (wave > 0) {
+        // ---------------- loader waves: wave q+1 keeps tile row ti-q cached ----------------
+        const int q = wave - 1;
+        while (!__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS)) {
+            const int cur = __hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS);
+            bool did = false;
+            if (cur >= 0) {
+                const int ti = cur >> 16, tj = cur & 0xffff;
+                for (int dc = 0; dc < 3 && !did; dc++) {
+                    const int tti = ti - q, ttj = tj - dc;
+                    if (tti < 0 || ttj < 0) continue;
+                    const int tg = (tti << 16) | ttj, sl = slot_of(tti, ttj);
+                    if (__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS) == tg) continue;
+                    if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_RELAXED, WGS);
+                    load_tile<CB>(w, tti, ttj, tiles[sl], sa[q], lane);
+                    const int now = __hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS);
+                    const int dti = (now >> 16) - tti, dtj = (now & 0xffff) - ttj;
+                    if (lane == 0 && dti >= 0 && dti <= 2 && dtj >= 0 && dtj <= 2)
+                        __hip_atomic_store(&tag[sl], tg, __ATOMIC_RELEASE, WGS);
+                    did = true;
+                }
+            }
+            if (!did) __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
+
+    // ---------------- walker wave ----------------
+    int i = m, j = n, L = 0, D = 0, h = 0, first = 1, reason = 3;
+    int ti = -1, tj = -1, sl = 0, nwait = 0, ntiles = 0;
+    const int maxh = m + n;
+    long long kb = 0;
+    unsigned rcur = lane < w.nrng ? w.rng[lane] : 0u;
+    unsigned rnxt = 64 + lane < w.nrng ? w.rng[64 + lane] : 0u;
     for (;;) {
-        if (st[6]) break;
-        const int ci = st[0], cj = st[1], k0 = st[3];
-        const int i0 = max(1, ci - WR + 1), j0 = max(1, cj - WC + 1);
-        __syncthreads();
-        // ---- stage the window: cells [i0, i0+WR) x [j0, j0+WC) ----
-        if (ci >= 1 && cj >= 1) {
-            for (int e = tid; e < WR * WC; e += blockDim.x) {
-                const int r = e / WC, cc = e - r * WC;
-                const int ii = i0 + r, jj = j0 + cc;
-                uint16_t v = 0;
-                if (ii <= m && jj <= n) v = (uint16_t)sets_from_code(tb_code(w.tb, w.CB, w.TC, ii, jj), w.CB, o);
-                win[e] = v;
-            }
-            for (int e = tid; e < WR; e += blockDim.x) wa[e] = (i0 + e <= m) ? w.a[i0 + e - 1] : 0;
-            for (int e = tid; e < WC; e += blockDim.x) wb[e] = (j0 + e <= n) ? w.b[j0 + e - 1] : 0;
-        }
-        for (int e = tid; e < RW; e += blockDim.x) wr[e] = (k0 + e < w.nrng) ? w.rng[k0 + e] : 0;
-        __syncthreads();
-        if (tid == 0) {
-            int i = st[0], j = st[1], L = st[2], D = st[3], h = st[4], first = st[5];
-            int done = 0, reason = 0;
-            const int maxh = m + n;
-            for (;;) {
-                if (D - k0 >= RW) break;  // restage the tie-break window
-                int S, am;
-                const bool inwin = i >= i0 && j >= j0 && i < i0 + WR && j < j0 + WC && ci >= 1 && cj >= 1;
-                if (inwin) {
-                    S = (win[(i - i0) * WC + (j - j0)] >> (3 * L)) & 7;
-                    am = wa[i - i0] == wb[j - j0];
-                } else if (i >= 1 && j >= 1) {
-                    break;  // interior cell outside the window: restage around it
-                } else {
-                    // degenerate walk at row 0 / column 0 with Python index wrapping
-                    const int ri = i < 0 ? i + m + 1 : i, rj = j < 0 ? j + n + 1 : j;
-                    const int pa = (i - 1) < 0 ? i - 1 + m : i - 1, pb = (j - 1) < 0 ? j - 1 + n : j - 1;
-                    if (ri < 0 || rj < 0 || pa < 0 || pa >= m || pb < 0 || pb >= n) {
-                        done = 1; reason = 4;  // IndexError
-                        break;
-                    }
-                    if (ri >= 1 && rj >= 1) {
-                        S = (sets_from_code(tb_code(w.tb, w.CB, w.TC, ri, rj), w.CB, o) >> (3 * L)) & 7;
-                    } else {
-                        const int* v = ri == 0 ? w.bnd_row + 3 * rj : w.bnd_col + 3 * ri;
-                        const long long M = v[0], X = v[1], Y = v[2];
-                        S = L == 0 ? argmin3(M, X, Y) : L == 1 ? argmin3(M + o, X, Y + o) : argmin3(M + o, X + o, Y);
-                    }
-                    am = w.a[pa] == w.b[pb];
+        int S, am;
+        if (i >= 1 && j >= 1) {
+            const int nti = (i - 1) >> 6, ntj = (j - 1) >> 6;
+            if (nti != ti || ntj != tj) {
+                ti = nti;
+                tj = ntj;
+                const int tg = (ti << 16) | tj;
+                sl = slot_of(ti, tj);
+                if (lane == 0) __hip_atomic_store(&cur_tile, tg, __ATOMIC_RELEASE, WGS);
+                ntiles++;
+                while (__hip_atomic_load(&tag[sl], __ATOMIC_ACQUIRE, WGS) != tg) {
+                    __builtin_amdgcn_s_sleep(1);
+                    nwait++;
                 }
-                const unsigned rb = wr[D - k0];
-                const int lvl = choose(S, am ? (rb & 31u) : (rb >> 5));
-                w.ops[D] = (uint8_t)lvl;
-                D++;
-                if (lvl == 0) { i--; j--; } else if (lvl == 1) { j--; } else { i--; }
-                L = lvl;
-                if (first) {
-                    first = 0;
-                    if (i == 0 && j == 0) { done = 1; reason = 0; break; }
-                    continue;
-                }
-                if (i == 0) { done = 1; reason = 1; break; }
-                if (j == 0) { done = 1; reason = 2; break; }
-                if (++h >= maxh) { done = 1; reason = 3; break; }
             }
-            st[0] = i; st[1] = j; st[2] = L; st[3] = D; st[4] = h; st[5] = first; st[6] = done; st[7] = reason;
-            if (done) { w.result[0] = D; w.result[1] = i; w.result[2] = j; w.result[3] = reason; }
+            const int v = tiles[sl][((i - 1) & 63) * TT + ((j - 1) & 63)];
+            S = (v >> (3 * L)) & 7;
+            am = (v >> 9) & 1;
+        } else {
+            // degenerate walk at row 0 / column 0 with Python index wrapping
+            const int ri = i < 0 ? i + m + 1 : i, rj = j < 0 ? j + n + 1 : j;
+            const int pa = (i - 1) < 0 ? i - 1 + m : i - 1, pb = (j - 1) < 0 ? j - 1 + n : j - 1;
+            if (ri < 0 || rj < 0 || pa < 0 || pa >= m || pb < 0 || pb >= n) { reason = 4; break; }  // IndexError
+            if (ri >= 1 && rj >= 1) {
+                S = (sets_from_code(tb_code(w.tb, CB, w.TC, ri, rj), CB, o) >> (3 * L)) & 7;
+            } else {
+                const int* vv = ri == 0 ? w.bnd_row + 3 * rj : w.bnd_col + 3 * ri;
+                const long long M = vv[0], X = vv[1], Y = vv[2];
+                S = L == 0 ? argmin3(M, X, Y) : L == 1 ? argmin3(M + o, X, Y + o) : argmin3(M + o, X + o, Y);
+            }
+            am = w.a[pa] == w.b[pb];
         }
-        __syncthreads();
+        while (D - kb >= 64) {  // next 64 entries of the tie-break table
+            kb += 64;
+            rcur = rnxt;
+            rnxt = kb + 64 + lane < w.nrng ? w.rng[kb + 64 + lane] : 0u;
+        }
+        const unsigned tab = __builtin_amdgcn_readlane(rcur, __builtin_amdgcn_readfirstlane((int)(D - kb)));
+        const int lvl = (int)(((am ? tab : (tab >> 14)) >> (2 * (S - 1))) & 3u);
+        w.ops[D] = (uint8_t)lvl;
+        D++;
+        i -= (lvl != 1);
+        j -= (lvl != 2);
+        L = lvl;
+        if (first) {
+            first = 0;
+            if (i == 0 && j == 0) { reason = 0; break; }
+            continue;
+        }
+        if (i == 0) { reason = 1; break; }
+        if (j == 0) { reason = 2; break; }
+        if (++h >= maxh) { reason = 3; break; }
+    }
+    if (lane == 0) {
+        w.result[0] = D; w.result[1] = i; w.result[2] = j; w.result[3] = reason;
+        w.result[4] = nwait; w.result[5] = ntiles;
+        __hip_atomic_store(&walk_done, 1, __ATOMIC_RELEASE, WGS);
     }
 }
 
 // ----------------------------------------------------------------------------------
 // host-side launchers (called from ga_host.cpp)
-void launch_qp(hipStream_t s, const uint8_t* a, int m, const int* sub, const int* gh, const int* gv, int K, void* qp,
-               long long stride, int qbytes) {
-    const long long total = stride * K;
-    int blocks = (int)min((total + 255) / 256, 4096LL);
-    if (qbytes == 1)
-        qp_kernel<int8_t><<<blocks, 256, 0, s>>>(a, m, sub, gh, gv, K, (int8_t*)qp, stride);
-    else
-        qp_kernel<int16_t><<<blocks, 256, 0, s>>>(a, m, sub, gh, gv, K, (int16_t*)qp, stride);
-}
-
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,
                      int o, int big, int* GVp, int* GHp, int2* top, int2* left, int* bnd_row, int* bnd_col, int* meta,
                      bool custom) {
@@ -522,12 +694,24 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
         boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, big, GVp, GHp, top, left, bnd_row, bnd_col, meta);
 }
 
+size_t fill_lds_bytes(int CB, int qbytes, bool tb, int K) {
+    const int spc = 16 / CB;
+    return (size_t)(tb ? FillLds::QRING_TB : FillLds::QRING_NOTB) + (size_t)K * (QROWS + spc) * qbytes;
+}
+
+template <int CB, typename QT, bool TB, bool FULL, int ABL>
+static void launch_one(hipStream_t s, const FillArgs& p) {
+    const size_t lds = fill_lds_bytes(CB, (int)sizeof(QT), TB, p.K);
+    auto* fn = fill_kernel<CB, QT, TB, FULL, ABL>;
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<dim3(p.nslabs), dim3(64 * (NW + 2)), lds, s>>>(p);
+}
+
 template <int CB, typename QT>
 static void launch_fill_t(hipStream_t s, const FillArgs& p, bool tb, bool full) {
-    dim3 grid(p.nslabs), block(64 * (NW + 1));
-    if (full) fill_kernel<CB, QT, true, true><<<grid, block, 0, s>>>(p);
-    else if (tb) fill_kernel<CB, QT, true, false><<<grid, block, 0, s>>>(p);
-    else fill_kernel<CB, QT, false, false><<<grid, block, 0, s>>>(p);
+    if (full) launch_one<CB, QT, true, true, 0>(s, p);
+    else if (tb) launch_one<CB, QT, true, false, 0>(s, p);
+    else launch_one<CB, QT, false, false, 0>(s, p);
 }
 
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full) {
@@ -542,6 +726,25 @@ void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, 
     }
 }
 
-void launch_walk(hipStream_t s, const WalkArgs& w) { walk_kernel<<<1, 256, 0, s>>>(w); }
+// diagnostic ablation launcher (CB=1, int8 profile only)
+void launch_fill_ablation(hipStream_t s, const FillArgs& p, bool tb, int abl) {
+#define GA_ABL_CASE(A)                                          \
+    case A:                                                     \
+        if (tb) launch_one<1, int8_t, true, false, A>(s, p);    \
+        else launch_one<1, int8_t, false, false, A>(s, p);      \
+        break;
+    switch (abl) {
+        GA_ABL_CASE(0) GA_ABL_CASE(1) GA_ABL_CASE(2) GA_ABL_CASE(4) GA_ABL_CASE(8) GA_ABL_CASE(16) GA_ABL_CASE(17)
+        GA_ABL_CASE(21) GA_ABL_CASE(29) GA_ABL_CASE(31)
+        default: break;
+    }
+#undef GA_ABL_CASE
+}
+
+void launch_walk(hipStream_t s, const WalkArgs& w) {
+    if (w.CB == 1) walk_kernel<1><<<1, 256, 0, s>>>(w);
+    else if (w.CB == 2) walk_kernel<2><<<1, 256, 0, s>>>(w);
+    else walk_kernel<4><<<1, 256, 0, s>>>(w);
+}
 
 }  // namespace ga

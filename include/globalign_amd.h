@@ -113,6 +113,8 @@ void* ga_ctx_stream(ga_ctx* ctx);
 /* Device time (ms, HIP events on the launch stream) of the last fill kernel
  * and of the last traceback walk kernel. */
 int ga_last_kernel_ms(ga_ctx* ctx, float* fill_ms, float* walk_ms);
+/* out4 = {fill kernel ms, walk kernel ms, host tie-break table ms, whole ga_problem_align wall ms}. */
+int ga_last_timings(ga_ctx* ctx, float* out4);
 
 #ifdef __cplusplus
 }

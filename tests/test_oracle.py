@@ -133,3 +133,22 @@ def test_mt_emulation_matches_cpython():
         core.lib().gao_mt_draws(st, len(sizes), sizes, got)
         assert got.tolist() == want
         assert state_digest(core.mt_state_tuple(st)) == state_digest()
+
+
+def test_pyport_matches_oracle():
+    """The CPU-baseline port (oracle/pyport.py) computes the same alignments as the oracle."""
+    from oracle import pyport
+    rng = random.Random(42)
+    for k in range(60):
+        s1 = "".join(rng.choice("ACGT") for _ in range(rng.randint(2, 60)))
+        s2 = "".join(rng.choice("ACGT") for _ in range(rng.randint(2, 60)))
+        kw = dict(seq_1=s1, seq_2=s2, match_score=2, mismatch_score=-3, gap_open_score=-rng.randint(0, 8),
+                  gap_extension_score=-1)
+        _, _, smat, cmat, gos, goc = transform.settings(kw)
+        random.seed(k)
+        ref = core.align(s1, s2, cmat, goc, core.mt_state_array())
+        random.seed(k)
+        T = pyport.fill(s1, s2, cmat, goc, transform.max_val(cmat))
+        a, mid, b, cost = pyport.traceback(T, s1, s2, cmat, goc)
+        assert cost == ref["cost"] and (a, mid, b) == ref["strings"]
+        assert state_digest() == state_digest(core.mt_state_tuple(ref["mt_out"]))
