@@ -102,26 +102,6 @@ struct PyMT {
     }
 };
 
-constexpr int SNAP = 1024;  // MT snapshots every SNAP dispatches
-
-// One dispatcher call = 18 draws of sizes [3,2,2,2,3,2,2,2,3] x {match, mismatch}
-// (the dict literal of cost_ranks_dispatcher, globaligner.py:598-672).  Only
-// draws 0-3 (match) and 9-12 (mismatch) can decide a move.  The step's entry
-// maps each candidate set S (bit k = level k is a minimum) to the level taken:
-// 2 bits at 2(S-1), match in bits 0-13, mismatch in bits 14-27.
-inline uint32_t dispatch_entry(PyMT& g) {
-    static const unsigned sizes[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
-    unsigned r[18];
-    for (int d = 0; d < 18; d++) r[d] = g.below(sizes[d]);
-    uint32_t e = 0;
-    for (int half = 0; half < 2; half++) {
-        const unsigned* q = r + 9 * half;
-        const unsigned lv[8] = {0, 0, 1, q[1], 2, 2 * q[2], 1 + q[3], q[0]};  // S = 1..7
-        for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * (S - 1) + 14 * half);
-    }
-    return e;
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ context
@@ -244,7 +224,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     HIPCHK(c->out_last.ensure(sizeof(int) * 4));
     HIPCHK(c->result.ensure(sizeof(int) * 8));
-    HIPCHK(c->ops.ensure(m + n_all + 8));
+    HIPCHK(c->ops.ensure(m + n_all + 1024));  // walk flushes whole 512-byte blocks
     HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->loaded = true;
@@ -357,23 +337,150 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-void build_rng(const uint32_t* state, int64_t steps, std::vector<uint32_t>& tab, std::vector<PyMT>& snaps) {
+// ---------------------------------------------------------------- tie-break table
+// The dispatcher's 18 draws per step consume a variable number of MT words
+// (getrandbits(2) with rejection: r >= size -> draw again).  The scan below
+// turns the word stream into the stream of ACCEPTED draws (18 per step) four
+// words at a time through a table indexed by (draw index mod 18, top-2-bit
+// quartet), then builds each step's entry from draws 0-3 / 9-12.
+struct QuadEntry {
+    uint32_t bytes;  // accepted values, one per byte, in order (unused bytes 0)
+    uint16_t meta;   // nacc (3 bits) | word offset of each acceptance (4 x 2 bits) << 3
+};
+struct Quad {
+    QuadEntry e[18][256];
+    Quad() {
+        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
+        for (int d = 0; d < 18; d++)
+            for (int B = 0; B < 256; B++) {
+                unsigned dd = d, nacc = 0, bytes = 0, pos = 0;
+                for (unsigned wi = 0; wi < 4; wi++) {
+                    const unsigned r = (B >> (2 * wi)) & 3u;
+                    if (r < sz[dd]) {
+                        bytes |= r << (8 * nacc);
+                        pos |= wi << (2 * nacc);
+                        nacc++;
+                        dd = (dd + 1) % 18;
+                    }
+                }
+                e[d][B].bytes = bytes;
+                e[d][B].meta = (uint16_t)(nacc | (pos << 3));
+            }
+    }
+};
+
+struct RngTable {
+    std::vector<uint32_t> tab;        // per dispatch: level per candidate set (see dispatch_entry)
+    std::vector<uint32_t> step_end;   // words consumed after each dispatch
+    std::vector<PyMT> twist_snap;     // MT array after every 64th twist (index 0 = initial state)
+    int mti0 = 0;
+};
+
+constexpr int TWSNAP = 64;
+
+inline void temper_block(const uint32_t* mt, uint32_t* out) {
+    for (int k = 0; k < MTN; k++) {
+        uint32_t y = mt[k];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        out[k] = y;
+    }
+}
+
+void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
+    static const Quad Q;
     PyMT g;
     std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
     g.mti = (int)state[MTN];
-    tab.resize(steps);
-    snaps.clear();
-    snaps.reserve(steps / SNAP + 1);
-    for (int64_t k = 0; k < steps; k++) {
-        if (k % SNAP == 0) snaps.push_back(g);
-        tab[k] = dispatch_entry(g);
+    R.mti0 = g.mti;
+    R.twist_snap.clear();
+    R.twist_snap.push_back(g);
+    R.tab.assign(steps, 0);
+    R.step_end.assign(steps, 0);
+    const int64_t need = 18 * steps;
+    std::vector<uint8_t> acc(need + 8);
+    uint32_t words[MTN + 4];
+    int64_t p = 0, wbase = 0, k = 0, ntw = 0;
+    unsigned d = 0;
+    // the partial first block: words mti0 .. 623 of the initial array
+    int first = g.mti, count = MTN - g.mti;
+    if (g.mti >= MTN) { count = 0; first = 0; }
+    uint32_t tmp[MTN];
+    temper_block(g.mt, tmp);
+    std::memcpy(words, tmp + first, sizeof(uint32_t) * count);
+    while (p < need) {
+        if (count == 0) {
+            g.twist();
+            ntw++;
+            if (ntw % TWSNAP == 0) R.twist_snap.push_back(g);
+            temper_block(g.mt, words);
+            count = MTN;
+        }
+        int q = 0;
+        for (; q + 4 <= count && p < need; q += 4) {
+            const unsigned B = (words[q] >> 30) | ((words[q + 1] >> 30) << 2) | ((words[q + 2] >> 30) << 4) |
+                               ((words[q + 3] >> 30) << 6);
+            const QuadEntry& e = Q.e[d][B];
+            const unsigned nacc = e.meta & 7u;
+            std::memcpy(acc.data() + p, &e.bytes, 4);
+            if (d + nacc >= 18) {  // the step completes inside this quartet
+                const unsigned t = 17 - d;
+                const int64_t st = (p + t) / 18;
+                if (st < steps) R.step_end[st] = (uint32_t)(wbase + q + ((e.meta >> (3 + 2 * t)) & 3u) + 1);
+            }
+            p += nacc;
+            d += nacc;
+            if (d >= 18) d -= 18;
+        }
+        // tail words of the block (count not a multiple of 4), one at a time
+        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
+        for (; q < count && p < need; q++) {
+            const unsigned r = words[q] >> 30;
+            if (r < sz[d]) {
+                acc[p] = (uint8_t)r;
+                if (d == 17) R.step_end[p / 18] = (uint32_t)(wbase + q + 1);
+                p++;
+                d = d == 17 ? 0 : d + 1;
+            }
+        }
+        wbase += count;
+        count = 0;
     }
-    if (steps % SNAP == 0) snaps.push_back(g);
+    (void)k;
+    for (int64_t st = 0; st < steps; st++) {
+        const uint8_t* r = acc.data() + 18 * st;
+        uint32_t e = 0;
+        for (int half = 0; half < 2; half++) {
+            const uint8_t* qq = r + 9 * half;
+            const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
+            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * (S - 1) + 14 * half);
+        }
+        R.tab[st] = e;
+    }
 }
 
-void state_after(const std::vector<PyMT>& snaps, int64_t D, uint32_t* out) {
-    PyMT g = snaps[D / SNAP];
-    for (int64_t k = 0; k < D % SNAP; k++) (void)dispatch_entry(g);
+// MT state after the first D dispatches consumed their words.
+void state_after(const RngTable& R, int64_t D, uint32_t* out) {
+    PyMT g = R.twist_snap[0];
+    if (D == 0) {
+        std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
+        out[MTN] = (uint32_t)g.mti;
+        return;
+    }
+    const int64_t W = R.step_end[D - 1];
+    const int64_t first = R.mti0 >= MTN ? 0 : MTN - R.mti0;
+    if (W <= first) {
+        g.mti = R.mti0 + (int)W;
+    } else {
+        const int64_t Wp = W - first;
+        const int64_t tw = (Wp + MTN - 1) / MTN;           // twists needed
+        const int64_t sidx = tw / TWSNAP;
+        g = R.twist_snap[sidx];
+        for (int64_t t = sidx * TWSNAP; t < tw; t++) g.twist();
+        g.mti = (int)(Wp - (tw - 1) * MTN);
+    }
     std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
     out[MTN] = (uint32_t)g.mti;
 }
@@ -404,7 +511,7 @@ int run_walk(ga_ctx* c, const std::vector<uint32_t>& tab) {
 
 inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 
-int finish_walk(ga_ctx* c, const std::vector<PyMT>& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
+int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
                 char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
     int res[8];
     HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 8, hipMemcpyDeviceToHost, c->stream));
@@ -519,11 +626,10 @@ int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const
     if (int r = check_ctx(c)) return r;
     if (!c->filled_tb) return fail(GA_E_STATE, "traceback needs a GA_FILL_TRACEBACK fill first");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
-    std::vector<uint32_t> tab;
-    std::vector<PyMT> snaps;
-    build_rng(mt_state, c->m + c->n + 1, tab, snaps);
-    if (int r = run_walk(c, tab)) return r;
-    return finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+    RngTable R;
+    build_rng(mt_state, c->m + c->n + 1, R);
+    if (int r = run_walk(c, R.tab)) return r;
+    return finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
 }
 
 int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
@@ -534,14 +640,13 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     const double t0 = now_ms();
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK)) return r;
     // the tie-break table is built on the host while the device fills
-    std::vector<uint32_t> tab;
-    std::vector<PyMT> snaps;
+    RngTable R;
     const double t1 = now_ms();
-    build_rng(mt_state, c->m + c->n + 1, tab, snaps);
+    build_rng(mt_state, c->m + c->n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
-    if (int r = run_walk(c, tab)) return r;
+    if (int r = run_walk(c, R.tab)) return r;
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
-    const int rc = finish_walk(c, snaps, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
+    const int rc = finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
     return rc;
 }
@@ -607,6 +712,20 @@ int ga_debug_stamps(ga_ctx* c, int enable, unsigned long long* out, int64_t cap)
         const int64_t nb = std::min<int64_t>(cap, 4 * (int64_t)c->nstripes);
         HIPCHK(hipMemcpy(out, c->dbg.p, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost));
     }
+    return GA_OK;
+}
+
+// CPU-only check of the tie-break table (tests): entries for `steps` dispatches from
+// the 625-word state, and the state after the first D of them.
+int ga_debug_rng(const uint32_t* state, int64_t steps, uint32_t* tab_out, int64_t D, uint32_t* state_out,
+                 double* ms_out) {
+    if (!state || !tab_out || !state_out || D < 0 || D > steps) return fail(GA_E_ARG, "bad argument");
+    RngTable R;
+    const double t0 = now_ms();
+    build_rng(state, steps, R);
+    if (ms_out) *ms_out = now_ms() - t0;
+    std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
+    state_after(R, D, state_out);
     return GA_OK;
 }
 

@@ -575,18 +575,57 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* dst, uint
     }
 }
 
+constexpr int RB = 2048;  // LDS rings of tie-break entries / chosen levels (4 blocks of 512 dispatches)
+
 template <int CB>
-__global__ void __launch_bounds__(256) walk_kernel(WalkArgs w) {
+__global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
     __shared__ uint16_t tiles[9][TT * TT];
+    __shared__ uint32_t rngbuf[RB];
+    __shared__ uint8_t opsbuf[RB];
     __shared__ uint8_t sa[3][TT];
     __shared__ int tag[9];
-    __shared__ int cur_tile;
-    __shared__ int walk_done;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ int rtag[4];
+    __shared__ int cur_tile, walk_done, wD, ops_flushed;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 9) tag[threadIdx.x] = -1;
-    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; }
+    if (threadIdx.x < 4) rtag[threadIdx.x] = -1;
+    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = 0; ops_flushed = 0; }
     __syncthreads();
     const int m = w.m, n = w.n, o = w.o;
+
+    if (wave == 4) {
+        // ---------------- helper: tie-break table HBM -> LDS ring, levels LDS ring -> HBM ----------------
+        const long long nblk = (w.nrng + 511) / 512;
+        long long rl = 0, fl = 0;
+        for (;;) {
+            const int d = __hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS);
+            const int done = __hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS);
+            bool moved = false;
+            while (rl < nblk && rl < (d >> 9) + 4) {
+                const long long e0 = rl * 512 + lane * 8;
+                uint32_t* dst = rngbuf + (rl & 3) * 512 + lane * 8;
+#pragma unroll
+                for (int k = 0; k < 8; k++) dst[k] = (e0 + k < w.nrng) ? w.rng[e0 + k] : 0u;
+                if (lane == 0) __hip_atomic_store(&rtag[rl & 3], (int)rl, __ATOMIC_RELEASE, WGS);
+                rl++;
+                moved = true;
+            }
+            const long long complete = done ? ((long long)d + 511) / 512 : (d >> 9);
+            while (fl < complete) {
+                const uint8_t* srcb = opsbuf + (fl & 3) * 512 + lane * 8;
+                uint8_t* dstb = w.ops + fl * 512 + lane * 8;
+#pragma unroll
+                for (int k = 0; k < 8; k++) dstb[k] = srcb[k];
+                fl++;
+                if (lane == 0) __hip_atomic_store(&ops_flushed, (int)fl, __ATOMIC_RELEASE, WGS);
+                moved = true;
+            }
+            if (done && fl >= complete) break;
+            if (!moved) __builtin_amdgcn_s_sleep(2);
+        }
+        return;
+    }
 
     if (wave > 0) {
         // ---------------- loader waves: wave q+1 keeps tile row ti-q cached ----------------
@@ -615,14 +654,20 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs w) {
         return;
     }
 
-    // ---------------- walker wave ----------------
+    // ---------------- walker wave (its loop touches LDS only) ----------------
     int i = m, j = n, L = 0, D = 0, h = 0, first = 1, reason = 3;
     int ti = -1, tj = -1, sl = 0, nwait = 0, ntiles = 0;
     const int maxh = m + n;
-    long long kb = 0;
-    unsigned rcur = lane < w.nrng ? w.rng[lane] : 0u;
-    unsigned rnxt = 64 + lane < w.nrng ? w.rng[64 + lane] : 0u;
     for (;;) {
+        if ((D & 511) == 0) {
+            // new block of 512 dispatches: its tie-break entries must be staged and the
+            // level slot it reuses (block - 4) flushed
+            const int blk = D >> 9;
+            if (lane == 0) __hip_atomic_store(&wD, D, __ATOMIC_RELEASE, WGS);
+            while (__hip_atomic_load(&rtag[blk & 3], __ATOMIC_ACQUIRE, WGS) != blk) __builtin_amdgcn_s_sleep(1);
+            while (__hip_atomic_load(&ops_flushed, __ATOMIC_ACQUIRE, WGS) < blk - 3) __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned tab = rngbuf[D & (RB - 1)];
         int S, am;
         if (i >= 1 && j >= 1) {
             const int nti = (i - 1) >> 6, ntj = (j - 1) >> 6;
@@ -655,14 +700,8 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs w) {
             }
             am = w.a[pa] == w.b[pb];
         }
-        while (D - kb >= 64) {  // next 64 entries of the tie-break table
-            kb += 64;
-            rcur = rnxt;
-            rnxt = kb + 64 + lane < w.nrng ? w.rng[kb + 64 + lane] : 0u;
-        }
-        const unsigned tab = __builtin_amdgcn_readlane(rcur, __builtin_amdgcn_readfirstlane((int)(D - kb)));
         const int lvl = (int)(((am ? tab : (tab >> 14)) >> (2 * (S - 1))) & 3u);
-        w.ops[D] = (uint8_t)lvl;
+        opsbuf[D & (RB - 1)] = (uint8_t)lvl;
         D++;
         i -= (lvl != 1);
         j -= (lvl != 2);
@@ -679,6 +718,7 @@ __global__ void __launch_bounds__(256) walk_kernel(WalkArgs w) {
     if (lane == 0) {
         w.result[0] = D; w.result[1] = i; w.result[2] = j; w.result[3] = reason;
         w.result[4] = nwait; w.result[5] = ntiles;
+        __hip_atomic_store(&wD, D, __ATOMIC_RELEASE, WGS);
         __hip_atomic_store(&walk_done, 1, __ATOMIC_RELEASE, WGS);
     }
 }
@@ -742,9 +782,9 @@ void launch_fill_ablation(hipStream_t s, const FillArgs& p, bool tb, int abl) {
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {
-    if (w.CB == 1) walk_kernel<1><<<1, 256, 0, s>>>(w);
-    else if (w.CB == 2) walk_kernel<2><<<1, 256, 0, s>>>(w);
-    else walk_kernel<4><<<1, 256, 0, s>>>(w);
+    if (w.CB == 1) walk_kernel<1><<<1, 320, 0, s>>>(w);
+    else if (w.CB == 2) walk_kernel<2><<<1, 320, 0, s>>>(w);
+    else walk_kernel<4><<<1, 320, 0, s>>>(w);
 }
 
 }  // namespace ga
