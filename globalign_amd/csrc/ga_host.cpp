@@ -125,7 +125,7 @@ struct ga_ctx {
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
     bool dbg_on = false;
     int ablation = -1;  // diagnostics: fill kernel ablation variant (-1 = product kernel)
-    int walk_waits = 0, walk_tiles = 0;
+    int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
     DevBuf dbg;
 };
 
@@ -223,8 +223,8 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
     HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     HIPCHK(c->out_last.ensure(sizeof(int) * 4));
-    HIPCHK(c->result.ensure(sizeof(int) * 8));
-    HIPCHK(c->ops.ensure(m + n_all + 1024));  // walk flushes whole 512-byte blocks
+    HIPCHK(c->result.ensure(sizeof(int) * 16));
+    HIPCHK(c->ops.ensure(m + n_all + 1024));  // 2-bit levels; the walk flushes whole 128-byte blocks
     HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->loaded = true;
@@ -455,7 +455,7 @@ void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
         for (int half = 0; half < 2; half++) {
             const uint8_t* qq = r + 9 * half;
             const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
-            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * (S - 1) + 14 * half);
+            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 16 * half);
         }
         R.tab[st] = e;
     }
@@ -513,16 +513,23 @@ inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 
 int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
                 char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
-    int res[8];
-    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 8, hipMemcpyDeviceToHost, c->stream));
+    int res[16];
+    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 16, hipMemcpyDeviceToHost, c->stream));
     c->walk_waits = res[4];
     c->walk_tiles = res[5];
+    c->walk_t_tile = res[6];
+    c->walk_t_ring = res[7];
+    c->walk_t_total = res[8];
+    c->walk_c_total = res[9];
+    c->walk_load_ticks = res[10];
+    c->walk_load_count = res[11];
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(&c->walk_ms, c->ev[2], c->ev[3]));
     const int64_t D = res[0];
     const int reason = res[3];
-    std::vector<uint8_t> ops(D);
-    if (D) HIPCHK(hipMemcpy(ops.data(), c->ops.p, D, hipMemcpyDeviceToHost));
+    // levels are packed 2 bits per dispatch, dispatch k at bits 30 - 2*(k & 15) of u32 word k >> 4
+    std::vector<uint32_t> ops((D + 15) / 16);
+    if (D) HIPCHK(hipMemcpy(ops.data(), c->ops.p, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     state_after(snaps, D, mt_state);
     if (reason == 4) {  // IndexError in the reference
         *tb_status = GA_TB_INDEX_ERROR;
@@ -537,8 +544,9 @@ int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char
     };
     for (int64_t k = 0; k < D; k++) {
         const char ca = a_chr[pywrap(i - 1, m)], cbb = b_chr[pywrap(j - 1, n)];
-        if (ops[k] == 0) { put(ca, ca == cbb ? '|' : '*', cbb); i--; j--; }
-        else if (ops[k] == 1) { put('-', ' ', cbb); j--; }
+        const unsigned lv = (ops[k >> 4] >> (30 - 2 * (k & 15))) & 3u;
+        if (lv == 0) { put(ca, ca == cbb ? '|' : '*', cbb); i--; j--; }
+        else if (lv == 1) { put('-', ' ', cbb); j--; }
         else { put(ca, ' ', '-'); i--; }
     }
     if (reason == 1)
@@ -735,10 +743,18 @@ int ga_debug_ablation(ga_ctx* c, int abl) {
     return GA_OK;
 }
 
-int ga_debug_walk(ga_ctx* c, int* out2) {
-    if (!c || !out2) return fail(GA_E_ARG, "null argument");
-    out2[0] = c->walk_waits;
-    out2[1] = c->walk_tiles;
+// out6 = {tile wait spins, tiles entered, tile-wait ticks, ring-wait ticks, walker ticks (100 MHz),
+//         walker shader clocks / 16, loader busy ticks, tiles loaded}
+int ga_debug_walk(ga_ctx* c, int* out5) {
+    if (!c || !out5) return fail(GA_E_ARG, "null argument");
+    out5[0] = c->walk_waits;
+    out5[1] = c->walk_tiles;
+    out5[2] = c->walk_t_tile;
+    out5[3] = c->walk_t_ring;
+    out5[4] = c->walk_t_total;
+    out5[5] = c->walk_c_total;
+    out5[6] = c->walk_load_ticks;
+    out5[7] = c->walk_load_count;
     return GA_OK;
 }
 

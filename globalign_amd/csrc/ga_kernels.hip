@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ga_device.h"
 
 namespace ga {
@@ -487,18 +489,33 @@ __global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
 // ----------------------------------------------------------------------------------
 // Traceback walk (dp_array_backward, globaligner.py:395-593).
 //
-// One workgroup of four waves.  Wave 0 walks; waves 1-3 keep a 3x3
-// direct-mapped cache of decoded 64x64 tiles (tile = 64 rows x one 64-column
-// stripe) filled ahead of the walker: the path is monotone (up/left), so the
-// tiles it can reach next are the 3x3 block above-left of its current tile,
-// and slot (ti mod 3, tj mod 3) gives every tile of that block its own slot.
-// A cached cell is a u16: rank sets S0|S1<<3|S2<<6 (see sets_from_code) and
-// bit 9 = (a_i == b_j).  The per-step tie-break choice comes from a host table
-// (two 7x2-bit maps from candidate set S to level, bits 2(S-1), for match and
-// mismatch), so a
-// step is: one LDS read, a shift and a mask.  Degenerate inputs (SURVEY A.5:
-// the walk visits row 0 / column 0 and wraps with Python negative indexing)
-// are reproduced cell by cell from HBM.
+// One workgroup of twelve waves.  Nine loader waves keep a 4x4 direct-mapped
+// cache of decoded 64x64 tiles (tile = 64 rows x one 64-column stripe) filled
+// ahead of the walker: the path is monotone (up/left), so the tiles it can
+// reach next are the 4x4 block above-left of its current tile.  The cache is a
+// 256x256 torus: cell (i, j) lives at ((i-1) mod 256, (j-1) mod 256), so every
+// tile of that block has its own place and any 8x8 window is two masks.
+// Wave 4 streams the host's tie-break table into an LDS ring and the chosen
+// levels back to HBM; wave 8 idles so the walker (wave 0) shares its SIMD with
+// the mostly-sleeping helper only.
+//
+// A cached cell is a u16 of three 5-bit shifts, one per entering level L:
+// sh_L = 2*S_L + 16*(a_i != b_j), S_L the rank set of sets_from_code.  The
+// host table entry of dispatch D holds, at bits sh..sh+1, the level the
+// reference's random.choice picks for that set (match half at 2S, mismatch
+// half at 16+2S), so a step is lvl = (tab >> sh_L) & 3.
+//
+// Wave 0 walks with scalar code only, in groups of 4 steps: each group issues
+// the LDS read of the 8x8 window anchored at its first cell (lane r*8+c =
+// cell (i-r, j-c), fields widened to bits 0/8/16) for the NEXT group -- a
+// window anchored at p covers every cell reachable from p in 7 steps -- and
+// each step reads its cell with v_readlane.  Four groups make an iteration of
+// 16 steps that runs without a single check when the walk is far from the
+// matrix edge and inside the tiles verified cached.  Chosen levels are packed
+// 2 bits per dispatch: dispatch D at bits 30 - 2*(D & 15) of u32 word D >> 4.
+// Degenerate walks (the walk visits row 0 / column 0 and wraps
+// with Python negative indexing) run a slower per-step path reproduced cell by
+// cell from HBM.
 
 __device__ __forceinline__ int argmin3(long long x, long long y, long long z) {
     long long h = x < y ? x : y;
@@ -521,6 +538,13 @@ __device__ __forceinline__ int sets_from_code(unsigned code, int CB, int o) {
     return (int)(S0 | (S1 << 3) | (S2 << 6));
 }
 
+// three 5-bit table shifts (one per entering level) from the rank sets and a_i == b_j
+__device__ __forceinline__ unsigned cell_shifts(int sets, bool am) {
+    const unsigned mm = am ? 0u : 16u;
+    const unsigned f0 = 2u * (sets & 7) + mm, f1 = 2u * ((sets >> 3) & 7) + mm, f2 = 2u * ((sets >> 6) & 7) + mm;
+    return f0 | (f1 << 5) | (f2 << 10);
+}
+
 __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, int i, int j) {
     const int s = (j - 1) >> 6, l = (j - 1) & 63, t = i - 1 + l;
     const int spc = 16 / CB;
@@ -531,15 +555,21 @@ __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, i
     return v;
 }
 
-constexpr int TT = 64;  // tile edge
+constexpr int TT = 64;       // tile edge
+constexpr int TB4 = 4;       // tile block edge (tiles cached per axis)
+constexpr int TP = TB4 * TT; // torus pitch (256)
+constexpr int NSLOT = TB4 * TB4;
 
-__device__ __forceinline__ int slot_of(int ti, int tj) { return (ti % 3) * 3 + (tj % 3); }
+__device__ __forceinline__ int slot_of(int ti, int tj) { return (ti & (TB4 - 1)) * TB4 + (tj & (TB4 - 1)); }
+__device__ __forceinline__ int torus_of(int i, int j) { return ((i - 1) & (TP - 1)) * TP + ((j - 1) & (TP - 1)); }
 
-// One loader wave decodes tile (ti, tj) into `dst`: lane = column; each lane
+// One loader wave decodes tile (ti, tj) into the torus: lane = column; each lane
 // walks the 16-byte chunks of its column's traceback stream that cover the
-// tile's 64 rows.
+// tile's 64 rows (the general path; one-byte words use load_tile_b1).
 template <int CB>
-__device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* dst, uint8_t* sa, int lane) {
+__device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
+                          int lane) {
+    uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT;
     constexpr int SPC = 16 / CB;
     constexpr int KMAX = TT / SPC + 1;
     const int i0 = ti * TT + 1;                       // first row of the tile
@@ -568,39 +598,109 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* dst, uint
                 unsigned code = wd[(u * CB) >> 2] >> ((u * CB * 8) & 31);
                 if (CB == 1) code &= 0xffu;
                 else if (CB == 2) code &= 0xffffu;
-                const int v = sets_from_code(code, CB, w.o) | ((int)(sa[r] == bj) << 9);
-                dst[r * TT + lane] = (uint16_t)v;
+                dst[r * TP + lane] = (uint16_t)cell_shifts(sets_from_code(code, CB, w.o), sa[r] == bj);
             }
         }
     }
 }
 
+// One-byte traceback words (the common case, gap open < 7): branch-free decode.
+// A lane's 64 cells sit at byte offset (tfirst mod 16) of the five 16-byte
+// chunks it loads; the lane realigns them (dword select + v_alignbyte), folds
+// a_i == b_j into bit 7 of each word (SWAR zero-byte test on the staged a
+// bytes; words use bits 0-6) and decodes through a 256-entry table.
+__device__ void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
+                             int lane) {
+    uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT + lane;
+    const int i0 = ti * TT + 1;
+    const int j = tj * TT + lane + 1;
+    sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
+    const bool colok = j <= w.n;
+    const unsigned bj = colok ? w.b[j - 1] : 0xfeu;
+    const int tfirst = i0 - 1 + lane;
+    const int q0 = tfirst >> 4, off = tfirst & 15;
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC) * 64 + lane;
+    unsigned wv[20];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const int q = q0 + k;
+        const uint4 c = (colok && q < w.TC) ? base[(long long)q * 64] : make_uint4(0, 0, 0, 0);
+        wv[4 * k] = c.x; wv[4 * k + 1] = c.y; wv[4 * k + 2] = c.z; wv[4 * k + 3] = c.w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
+    __builtin_amdgcn_wave_barrier();
+    const uint4* sa4 = reinterpret_cast<const uint4*>(sa);
+    unsigned av[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint4 x = sa4[k];
+        av[4 * k] = x.x; av[4 * k + 1] = x.y; av[4 * k + 2] = x.z; av[4 * k + 3] = x.w;
+    }
+    const int dw = off >> 2;
+    const unsigned sb = (unsigned)(off & 3);
+    unsigned al[17];
+#pragma unroll
+    for (int k = 0; k < 17; k++) al[k] = dw == 0 ? wv[k] : dw == 1 ? wv[k + 1] : dw == 2 ? wv[k + 2] : wv[k + 3];
+    const unsigned bj4 = bj * 0x01010101u;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        unsigned cw = __builtin_amdgcn_alignbyte(al[k + 1], al[k], sb);  // rows 4k .. 4k+3
+        const unsigned x = av[k] ^ bj4;
+        const unsigned t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;      // bit 7 of a byte clear <=> byte == 0
+        cw = (cw & 0x7f7f7f7fu) | (~t & 0x80808080u);
+#pragma unroll
+        for (int u = 0; u < 4; u++) dst[(4 * k + u) * TP] = lut[(cw >> (8 * u)) & 0xffu];
+    }
+}
+
 constexpr int RB = 2048;  // LDS rings of tie-break entries / chosen levels (4 blocks of 512 dispatches)
 
+__device__ __forceinline__ int sgpr(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Waves: 0 walker, 4 ring helper, 8 idle (so the walker's SIMD runs nothing
+// else), the other nine load tiles.
+constexpr int WALK_WAVES = 12;
+constexpr int NLOAD = 9;
+// loader claim order over the 4x4 block: nearest tiles first (row offset, column offset)
+__constant__ int8_t LOAD_ORDER[NSLOT][2] = {{0, 0}, {1, 0}, {0, 1}, {1, 1}, {2, 0}, {0, 2}, {2, 1}, {1, 2},
+                                           {2, 2}, {3, 0}, {0, 3}, {3, 1}, {1, 3}, {3, 2}, {2, 3}, {3, 3}};
+
+__device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
+    const int dti = (cur >> 16) - ti, dtj = (cur & 0xffff) - tj;
+    return cur >= 0 && dti >= 0 && dti < TB4 && dtj >= 0 && dtj < TB4;
+}
+
 template <int CB>
-__global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
-    __shared__ uint16_t tiles[9][TT * TT];
-    __shared__ uint32_t rngbuf[RB];
-    __shared__ uint8_t opsbuf[RB];
-    __shared__ uint8_t sa[3][TT];
-    __shared__ int tag[9];
+__global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
+    __shared__ uint16_t torus[TP * TP];
+    __shared__ __attribute__((aligned(16))) uint32_t rngbuf[RB];
+    __shared__ uint32_t opsbuf[RB / 16];
+    __shared__ uint16_t lut[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD][TT];
+    __shared__ int tag[NSLOT], busy[NSLOT];
     __shared__ int rtag[4];
     __shared__ int cur_tile, walk_done, wD, ops_flushed;
+    __shared__ unsigned long long load_ticks;
+    __shared__ int load_count;
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < 9) tag[threadIdx.x] = -1;
+    const int wave = sgpr(threadIdx.x >> 6);
+    const int m = w.m, n = w.n, o = w.o;
+    if (threadIdx.x == 0) { load_ticks = 0; load_count = 0; }
+    if (threadIdx.x < NSLOT) { tag[threadIdx.x] = -1; busy[threadIdx.x] = 0; }
     if (threadIdx.x < 4) rtag[threadIdx.x] = -1;
     if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = 0; ops_flushed = 0; }
+    if (CB == 1 && threadIdx.x < 256)
+        lut[threadIdx.x] = (uint16_t)cell_shifts(sets_from_code(threadIdx.x & 127u, 1, o), (threadIdx.x >> 7) != 0);
     __syncthreads();
-    const int m = w.m, n = w.n, o = w.o;
 
+    if (wave == 8) return;
     if (wave == 4) {
         // ---------------- helper: tie-break table HBM -> LDS ring, levels LDS ring -> HBM ----------------
         const long long nblk = (w.nrng + 511) / 512;
         long long rl = 0, fl = 0;
         for (;;) {
-            const int d = __hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS);
-            const int done = __hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS);
+            const int d = sgpr(__hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS));
+            const int done = sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS));
             bool moved = false;
             while (rl < nblk && rl < (d >> 9) + 4) {
                 const long long e0 = rl * 512 + lane * 8;
@@ -612,41 +712,60 @@ __global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
                 moved = true;
             }
             const long long complete = done ? ((long long)d + 511) / 512 : (d >> 9);
-            while (fl < complete) {
-                const uint8_t* srcb = opsbuf + (fl & 3) * 512 + lane * 8;
-                uint8_t* dstb = w.ops + fl * 512 + lane * 8;
-#pragma unroll
-                for (int k = 0; k < 8; k++) dstb[k] = srcb[k];
+            while (fl < complete) {  // 512 dispatches = 32 words of levels
+                if (lane < 32) reinterpret_cast<uint32_t*>(w.ops)[fl * 32 + lane] = opsbuf[(fl & 3) * 32 + lane];
                 fl++;
                 if (lane == 0) __hip_atomic_store(&ops_flushed, (int)fl, __ATOMIC_RELEASE, WGS);
                 moved = true;
             }
             if (done && fl >= complete) break;
-            if (!moved) __builtin_amdgcn_s_sleep(2);
+            if (!moved) __builtin_amdgcn_s_sleep(8);
         }
         return;
     }
 
     if (wave > 0) {
-        // ---------------- loader waves: wave q+1 keeps tile row ti-q cached ----------------
-        const int q = wave - 1;
-        while (!__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS)) {
-            const int cur = __hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS);
+        // ---------------- loader pool: claim the nearest uncached tile of the walker's 4x4 block ----------------
+        // A slot is written only by the loader holding busy[slot].  The claim re-reads the current tile
+        // after invalidating the slot's tag, so a tile the walker may still read is never overwritten:
+        // the walker publishes its tile before it checks a tag.
+        const int li = wave - 1 - (wave > 4) - (wave > 8);
+        while (!sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS))) {
+            const int cur = sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS));
             bool did = false;
             if (cur >= 0) {
                 const int ti = cur >> 16, tj = cur & 0xffff;
-                for (int dc = 0; dc < 3 && !did; dc++) {
-                    const int tti = ti - q, ttj = tj - dc;
+                for (int pidx = 0; pidx < NSLOT && !did; pidx++) {
+                    const int tti = ti - LOAD_ORDER[pidx][0], ttj = tj - LOAD_ORDER[pidx][1];
                     if (tti < 0 || ttj < 0) continue;
                     const int tg = (tti << 16) | ttj, sl = slot_of(tti, ttj);
-                    if (__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS) == tg) continue;
-                    if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_RELAXED, WGS);
-                    load_tile<CB>(w, tti, ttj, tiles[sl], sa[q], lane);
-                    const int now = __hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS);
-                    const int dti = (now >> 16) - tti, dtj = (now & 0xffff) - ttj;
-                    if (lane == 0 && dti >= 0 && dti <= 2 && dtj >= 0 && dtj <= 2)
-                        __hip_atomic_store(&tag[sl], tg, __ATOMIC_RELEASE, WGS);
-                    did = true;
+                    if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
+                    if (sgpr(__hip_atomic_load(&busy[sl], __ATOMIC_RELAXED, WGS)) != 0) continue;
+                    int got = 0;
+                    if (lane == 0) {
+                        int expect = 0;
+                        got = __hip_atomic_compare_exchange_strong(&busy[sl], &expect, 1, __ATOMIC_SEQ_CST,
+                                                                   __ATOMIC_RELAXED, WGS);
+                    }
+                    if (!sgpr(got)) continue;
+                    bool ok = sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_SEQ_CST, WGS)) != tg;
+                    if (ok) {
+                        if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_SEQ_CST, WGS);
+                        ok = in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj);
+                    }
+                    if (ok) {
+                        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                        if (CB == 1) load_tile_b1(w, tti, ttj, torus, sa[li], lut, lane);
+                        else load_tile<CB>(w, tti, ttj, torus, sa[li], lut, lane);
+                        if (lane == 0) {
+                            atomicAdd(&load_ticks, __builtin_amdgcn_s_memrealtime() - t0);
+                            atomicAdd(&load_count, 1);
+                        }
+                        if (lane == 0 && in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj))
+                            __hip_atomic_store(&tag[sl], tg, __ATOMIC_RELEASE, WGS);
+                        did = true;
+                    }
+                    if (lane == 0) __hip_atomic_store(&busy[sl], 0, __ATOMIC_RELEASE, WGS);
                 }
             }
             if (!did) __builtin_amdgcn_s_sleep(2);
@@ -655,42 +774,71 @@ __global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
     }
 
     // ---------------- walker wave (its loop touches LDS only) ----------------
-    int i = m, j = n, L = 0, D = 0, h = 0, first = 1, reason = 3;
-    int ti = -1, tj = -1, sl = 0, nwait = 0, ntiles = 0;
+    int i = m, j = n, L = 0, D = 0, h = 0, first = 1, reason = -1;
+    int cti = -1, ctj = -1, nwait = 0, ntiles = 0;
     const int maxh = m + n;
-    for (;;) {
-        if ((D & 511) == 0) {
-            // new block of 512 dispatches: its tie-break entries must be staged and the
-            // level slot it reuses (block - 4) flushed
-            const int blk = D >> 9;
-            if (lane == 0) __hip_atomic_store(&wD, D, __ATOMIC_RELEASE, WGS);
-            while (__hip_atomic_load(&rtag[blk & 3], __ATOMIC_ACQUIRE, WGS) != blk) __builtin_amdgcn_s_sleep(1);
-            while (__hip_atomic_load(&ops_flushed, __ATOMIC_ACQUIRE, WGS) < blk - 3) __builtin_amdgcn_s_sleep(1);
+    unsigned long long t_tile = 0, t_ring = 0;  // time spent waiting (s_memrealtime ticks, 100 MHz)
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();
+    // make tile (ti, tj) current for the loaders (publish) and wait until it is cached
+    auto need_tile = [&](int ti, int tj, bool publish) {
+        const int tg = (ti << 16) | tj;
+        if (publish && lane == 0) __hip_atomic_store(&cur_tile, tg, __ATOMIC_SEQ_CST, WGS);
+        const int sl = slot_of(ti, tj);
+        if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_SEQ_CST, WGS)) == tg) return;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_ACQUIRE, WGS)) != tg) {
+            __builtin_amdgcn_s_sleep(1);
+            nwait++;
         }
-        const unsigned tab = rngbuf[D & (RB - 1)];
-        int S, am;
+        t_tile += __builtin_amdgcn_s_memrealtime() - t0;
+    };
+    // a new block of 512 dispatches: the level slot it reuses (block - 4) must be flushed
+    auto block_start = [&](int d) {
+        const int blk = d >> 9;
+        if (lane == 0) __hip_atomic_store(&wD, d, __ATOMIC_RELEASE, WGS);
+        if (sgpr(__hip_atomic_load(&ops_flushed, __ATOMIC_ACQUIRE, WGS)) >= blk - 3) return;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (sgpr(__hip_atomic_load(&ops_flushed, __ATOMIC_ACQUIRE, WGS)) < blk - 3) __builtin_amdgcn_s_sleep(1);
+        t_ring += __builtin_amdgcn_s_memrealtime() - t0;
+    };
+    auto rng_ready = [&](int d) {
+        const int blk = d >> 9;
+        if (sgpr(__hip_atomic_load(&rtag[blk & 3], __ATOMIC_ACQUIRE, WGS)) == blk) return;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (sgpr(__hip_atomic_load(&rtag[blk & 3], __ATOMIC_ACQUIRE, WGS)) != blk) __builtin_amdgcn_s_sleep(1);
+        t_ring += __builtin_amdgcn_s_memrealtime() - t0;
+    };
+    // the byte of the level word that holds dispatches 4*(d/4) .. +3 (little-endian u32 words)
+    auto ops_byte = [&](int d) -> uint8_t* {
+        return reinterpret_cast<uint8_t*>(opsbuf) + (((d >> 4) & (RB / 16 - 1)) * 4 + 3 - ((d >> 2) & 3));
+    };
+
+    // ---- per-step path: the first moves, and degenerate walks, until the walk is in the
+    //      interior at a dispatch count that is a multiple of 16 ----
+    for (;;) {
+        if (!first && i >= 1 && j >= 1 && (D & 15) == 0) break;
+        if ((D & 511) == 0) {
+            block_start(D);
+            rng_ready(D);
+        }
+        const unsigned tab = (unsigned)sgpr((int)rngbuf[D & (RB - 1)]);
+        unsigned sh;
         if (i >= 1 && j >= 1) {
             const int nti = (i - 1) >> 6, ntj = (j - 1) >> 6;
-            if (nti != ti || ntj != tj) {
-                ti = nti;
-                tj = ntj;
-                const int tg = (ti << 16) | tj;
-                sl = slot_of(ti, tj);
-                if (lane == 0) __hip_atomic_store(&cur_tile, tg, __ATOMIC_RELEASE, WGS);
+            if (nti != cti || ntj != ctj) {
+                cti = nti;
+                ctj = ntj;
                 ntiles++;
-                while (__hip_atomic_load(&tag[sl], __ATOMIC_ACQUIRE, WGS) != tg) {
-                    __builtin_amdgcn_s_sleep(1);
-                    nwait++;
-                }
+                need_tile(cti, ctj, true);
             }
-            const int v = tiles[sl][((i - 1) & 63) * TT + ((j - 1) & 63)];
-            S = (v >> (3 * L)) & 7;
-            am = (v >> 9) & 1;
+            sh = ((unsigned)sgpr(torus[torus_of(i, j)]) >> (5 * L)) & 31u;
         } else {
             // degenerate walk at row 0 / column 0 with Python index wrapping
             const int ri = i < 0 ? i + m + 1 : i, rj = j < 0 ? j + n + 1 : j;
             const int pa = (i - 1) < 0 ? i - 1 + m : i - 1, pb = (j - 1) < 0 ? j - 1 + n : j - 1;
             if (ri < 0 || rj < 0 || pa < 0 || pa >= m || pb < 0 || pb >= n) { reason = 4; break; }  // IndexError
+            int S;
             if (ri >= 1 && rj >= 1) {
                 S = (sets_from_code(tb_code(w.tb, CB, w.TC, ri, rj), CB, o) >> (3 * L)) & 7;
             } else {
@@ -698,10 +846,11 @@ __global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
                 const long long M = vv[0], X = vv[1], Y = vv[2];
                 S = L == 0 ? argmin3(M, X, Y) : L == 1 ? argmin3(M + o, X, Y + o) : argmin3(M + o, X + o, Y);
             }
-            am = w.a[pa] == w.b[pb];
+            sh = (unsigned)sgpr((int)(2u * S + (w.a[pa] == w.b[pb] ? 0u : 16u)));
         }
-        const int lvl = (int)(((am ? tab : (tab >> 14)) >> (2 * (S - 1))) & 3u);
-        opsbuf[D & (RB - 1)] = (uint8_t)lvl;
+        const int lvl = (int)((tab >> sh) & 3u);
+        uint8_t* ob = ops_byte(D);
+        *ob = (uint8_t)(((D & 3) ? *ob : 0) | (lvl << (6 - 2 * (D & 3))));
         D++;
         i -= (lvl != 1);
         j -= (lvl != 2);
@@ -715,9 +864,128 @@ __global__ void __launch_bounds__(320) walk_kernel(WalkArgs w) {
         if (j == 0) { reason = 2; break; }
         if (++h >= maxh) { reason = 3; break; }
     }
+
+    if (reason < 0) {
+        // ---- scalar interior walk (i, j >= 1; every move lowers i + j, so it ends at i == 0 or j == 0) ----
+        const int lr = lane >> 3, lc = lane & 7;
+        int vlo_i = 1 << 30, vlo_j = 1 << 30;  // lowest row / column of the verified tiles
+        // verify the tile of (pi, pj) and its neighbours above / to the left (2x2 tiles): every window
+        // anchored at least 20 rows and columns inside them is then cached
+        auto verify = [&](int pi, int pj) {
+            const int thi = (pi - 1) >> 6, thj = (pj - 1) >> 6;
+            const int tli = max(thi - 1, 0), tlj = max(thj - 1, 0);
+            const bool moved = thi != cti || thj != ctj;
+            if (moved) ntiles++;
+            need_tile(thi, thj, moved);
+            if (tlj != thj) need_tile(thi, tlj, false);
+            if (tli != thi) {
+                need_tile(tli, thj, false);
+                if (tlj != thj) need_tile(tli, tlj, false);
+            }
+            cti = thi;
+            ctj = thj;
+            vlo_i = tli == 0 ? -(1 << 30) : tli * TT + 1;
+            vlo_j = tlj == 0 ? -(1 << 30) : tlj * TT + 1;
+        };
+        // one LDS read per lane: the 8x8 window anchored at (pi, pj)
+        // (cells above row 1 / left of column 1 wrap round the torus and are never used)
+        auto window = [&](int pi, int pj) -> int {
+            const unsigned r = (unsigned)(pi - 1 - lr) & (TP - 1), c = (unsigned)(pj - 1 - lc) & (TP - 1);
+            return torus[r * TP + c];
+        };
+        // widen a window cell when its group starts: the empty asm keeps the compiler from pulling the
+        // widening (and so the wait for the LDS read) back into the group that issued the read
+        auto widen = [](int raw) -> int {
+            asm volatile("" : "+v"(raw));
+            const unsigned u = (unsigned)raw;
+            return (int)((u & 31u) | ((u & 0x3e0u) << 3) | ((u & 0x7c00u) << 6));
+        };
+        auto tabs = [&](int d) { return *reinterpret_cast<const uint4*>(rngbuf + (d & (RB - 1))); };
+
+        if ((D & 511) == 0) {
+            block_start(D);
+            rng_ready(D);
+        }
+        verify(i, j);
+        int wnext = window(i, j);    // anchored at the walk's current cell
+        uint4 tnext = tabs(D);
+        unsigned rel = 0;            // offset of the current cell from wnext's anchor (di*8 + dj)
+        unsigned L8 = 8u * L;        // bit offset of the entering level's field in a window cell
+        unsigned ops = 0;
+
+        // One group of 4 steps: swap in the prefetched window and entries, prefetch the next ones.
+        // CHECK: stop at the matrix edge; returns the steps taken when the walk ended, else 0.
+        auto group = [&](auto check_tag, int gd) -> int {  // gd: dispatch of the group's first step
+            constexpr bool CHECK = decltype(check_tag)::value;
+            const int wcur = widen(wnext);
+            const uint4 tc = tnext;
+            wnext = window(i, j);
+            tnext = tabs(gd + 4);
+            __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
+            const unsigned t[4] = {(unsigned)sgpr((int)tc.x), (unsigned)sgpr((int)tc.y), (unsigned)sgpr((int)tc.z),
+                                   (unsigned)sgpr((int)tc.w)};
+            unsigned idx = rel, mv = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)(idx + mv));
+                const unsigned lvl = (t[k] >> ((v >> L8) & 31u)) & 3u;
+                ops = ops * 4u + lvl;
+                L8 = lvl << 3;
+                mv += (0x080109u >> L8) & 0xffu;  // diag 9, left 1, up 8
+                if (CHECK) {
+                    if ((int)(mv >> 3) == i || (int)(mv & 7u) == j) {
+                        i -= (int)(mv >> 3);
+                        j -= (int)(mv & 7u);
+                        return k + 1;
+                    }
+                }
+            }
+            i -= (int)(mv >> 3);
+            j -= (int)(mv & 7u);
+            rel = mv;
+            return 0;
+        };
+        for (;;) {
+            // iteration of 16 dispatches D .. D+15 (D % 16 == 0)
+            if ((D & 511) == 0) block_start(D);
+            if (((D + 16) & 511) == 0) rng_ready(D + 16);
+            // every window of this iteration is anchored within 12 steps: rows >= i - 19
+            if (__builtin_expect(i - 19 < vlo_i || j - 19 < vlo_j, 0)) verify(i, j);
+            if (__builtin_expect(min(i, j) > 16, 1)) {
+                group(std::false_type{}, D);
+                group(std::false_type{}, D + 4);
+                group(std::false_type{}, D + 8);
+                group(std::false_type{}, D + 12);
+                opsbuf[(D >> 4) & (RB / 16 - 1)] = ops;
+                D += 16;
+                continue;
+            }
+            // near the top / left edge (the verified tiles reach row / column 1 here)
+            int g = 0, k = 0;
+            for (; g < 4; g++) {
+                k = group(std::true_type{}, D + 4 * g);
+                if (k) break;
+            }
+            if (g < 4) {
+                // ended after k steps of group g: left-align the partial word
+                const int nd = 4 * g + k;
+                opsbuf[(D >> 4) & (RB / 16 - 1)] = ops << (2 * (16 - nd));
+                D += nd;
+                reason = i == 0 ? 1 : 2;
+                break;
+            }
+            opsbuf[(D >> 4) & (RB / 16 - 1)] = ops;
+            D += 16;
+        }
+    }
     if (lane == 0) {
         w.result[0] = D; w.result[1] = i; w.result[2] = j; w.result[3] = reason;
         w.result[4] = nwait; w.result[5] = ntiles;
+        w.result[6] = (int)t_tile; w.result[7] = (int)t_ring;
+        w.result[8] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
+        w.result[9] = (int)((__builtin_amdgcn_s_memtime() - c_start) >> 4);
+        w.result[10] = (int)load_ticks;  // loaders still running only finish tiles nobody waits for
+        w.result[11] = load_count;
         __hip_atomic_store(&wD, D, __ATOMIC_RELEASE, WGS);
         __hip_atomic_store(&walk_done, 1, __ATOMIC_RELEASE, WGS);
     }
@@ -782,9 +1050,9 @@ void launch_fill_ablation(hipStream_t s, const FillArgs& p, bool tb, int abl) {
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {
-    if (w.CB == 1) walk_kernel<1><<<1, 320, 0, s>>>(w);
-    else if (w.CB == 2) walk_kernel<2><<<1, 320, 0, s>>>(w);
-    else walk_kernel<4><<<1, 320, 0, s>>>(w);
+    if (w.CB == 1) walk_kernel<1><<<1, 64 * WALK_WAVES, 0, s>>>(w);
+    else if (w.CB == 2) walk_kernel<2><<<1, 64 * WALK_WAVES, 0, s>>>(w);
+    else walk_kernel<4><<<1, 64 * WALK_WAVES, 0, s>>>(w);
 }
 
 }  // namespace ga
