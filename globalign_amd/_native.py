@@ -40,9 +40,23 @@ class EngineError(RuntimeError):
 # every symbol include/globalign_amd.h declares (tests check the exports)
 EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill",
-    "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_fill_launch",
-    "ga_slab_fill_finish", "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms", "ga_last_timings",
+    "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
+    "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
+    "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms", "ga_last_timings",
 ]
+
+
+class WalkState(C.Structure):
+    """ga_walk_state: the traceback walk handed from slab to slab (right to left)."""
+    _fields_ = [("i", C.c_int64), ("j", C.c_int64), ("D", C.c_int64), ("h", C.c_int64), ("L", C.c_int32),
+                ("first", C.c_int32), ("reason", C.c_int32), ("pad", C.c_int32)]
+
+    def as_list(self):
+        return [self.i, self.j, self.D, self.h, self.L, self.first, self.reason]
+
+    @classmethod
+    def from_list(cls, v):
+        return cls(int(v[0]), int(v[1]), int(v[2]), int(v[3]), int(v[4]), int(v[5]), int(v[6]), 0)
 
 
 def _preload_hip_runtime():
@@ -91,6 +105,11 @@ def load_library():
                                        pi64, p32, pi64]
         L.ga_problem_set_slab.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), i64, i64]
         L.ga_slab_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
+        L.ga_slab_bind_halos.argtypes = [vp, vp, vp]
+        L.ga_slab_walk_prepare.argtypes = [vp, pu32]
+        L.ga_slab_walk.argtypes = [vp, C.POINTER(WalkState), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                   C.c_char_p, i64, pi64]
+        L.ga_slab_mt_state.argtypes = [vp, i64, pu32]
         L.ga_slab_fill_launch.argtypes = [vp, i32]
         L.ga_slab_fill_finish.argtypes = [vp, pi64]
         L.ga_stream_wait_ge.argtypes = [vp, vp, C.c_uint32]
@@ -231,18 +250,53 @@ class Engine:
         self.m, self.n = len(a_codes), int(col_end - col_begin)
 
     def slab_buffers(self):
+        """-> (halo_in device ptr, halo_in_prog HOST ptr, halo_out device ptr, halo_out_prog HOST ptr)"""
         vp = C.c_void_p
         hi, hip_, ho, hop = vp(), vp(), vp(), vp()
         _check(self._L.ga_slab_buffers(self._h, C.byref(hi), C.byref(hip_), C.byref(ho), C.byref(hop)))
+        self._in_prog = C.c_uint32.from_address(hip_.value)
+        self._out_prog = C.c_uint32.from_address(hop.value)
         return hi.value, hip_.value, ho.value, hop.value
+
+    def slab_bind_halos(self, halo_in_ptr, halo_out_ptr):
+        """Use caller-owned (m+1) x int2 buffers (device or pinned host memory) as the slab's edges."""
+        _check(self._L.ga_slab_bind_halos(self._h, C.c_void_p(halo_in_ptr), C.c_void_p(halo_out_ptr)))
 
     def slab_launch(self, traceback=False):
         _check(self._L.ga_slab_fill_launch(self._h, GA_FILL_TRACEBACK if traceback else 0))
+        self.slab_buffers()
 
     def slab_finish(self):
         cost = C.c_int64(0)
         _check(self._L.ga_slab_fill_finish(self._h, C.byref(cost)))
         return cost.value
+
+    # progress words of the running slab fill (pinned host memory shared with the kernel)
+    def out_progress(self):
+        return self._out_prog.value
+
+    def set_in_progress(self, rows):
+        self._in_prog.value = int(rows)
+
+    def slab_walk_prepare(self, mt_words):
+        mt = np.ascontiguousarray(mt_words, dtype=np.uint32)
+        _check(self._L.ga_slab_walk_prepare(self._h, mt.ctypes.data_as(C.POINTER(C.c_uint32))))
+
+    def slab_walk(self, state, a_chr, b_chr):
+        """Continue the walk (list state, see WalkState) on this slab -> (segment strings, new state)."""
+        st = WalkState.from_list(state)
+        cap = self.m + 2 * len(b_chr) + 2
+        oa, om, ob = C.create_string_buffer(cap), C.create_string_buffer(cap), C.create_string_buffer(cap)
+        ln = C.c_int64(0)
+        _check(self._L.ga_slab_walk(self._h, C.byref(st), a_chr.encode(), b_chr.encode(), oa, om, ob, cap,
+                                    C.byref(ln)))
+        n = ln.value
+        return (oa.raw[:n].decode(), om.raw[:n].decode(), ob.raw[:n].decode()), st.as_list()
+
+    def slab_mt_state(self, D):
+        out = np.zeros(625, dtype=np.uint32)
+        _check(self._L.ga_slab_mt_state(self._h, int(D), out.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return out
 
     def stream(self):
         return self._L.ga_ctx_stream(self._h)

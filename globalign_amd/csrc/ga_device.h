@@ -29,6 +29,7 @@ struct FillArgs {
     uint8_t* tb;              // traceback words or nullptr
     int* out_last;            // [4]: H'(m, n_local)
     unsigned* edge_prog;      // rows of the right edge published (last slab only; may be null)
+    int2* edge_out;           // right edge of the last workgroup slab (nullptr: its hand slot)
     int* full;                // FULL output (shifted M', X', Y') or nullptr
     int m, n, o, nstripes, nslabs, TC;
     unsigned spin_limit, halo_spin_limit;
@@ -39,14 +40,17 @@ struct WalkArgs {
     const uint8_t* tb;
     int CB, TC;
     const uint8_t* a;
-    const uint8_t* b;
+    const uint8_t* b;     // this slab's columns
     const int* bnd_row;   // 3(n+1) original boundary triples
     const int* bnd_col;   // 3(m+1)
-    const uint32_t* rng;  // per dispatch: level chosen for each candidate set (match | mismatch<<14)
+    const uint32_t* rng;  // per dispatch: level chosen for candidate set S at bits 2S (match) / 16+2S (mismatch)
     long long nrng;
-    int m, n, o;
-    uint8_t* ops;         // out: chosen level per dispatch
-    int* result;          // out: [D, i, j, reason]
+    int m, n, o;          // n: this slab's columns
+    int i0, j0, L0, first0, D0, h0;  // start state (j0 local); a whole problem starts at (m, n, 0, 1, 0, 0)
+    int handoff;          // 1: the slab has columns to its left; reaching local column 0 ends the walk here
+    int maxh;             // the reference's move bound m + n (global n)
+    uint32_t* ops;        // out: 2-bit levels, dispatch D at bits 30 - 2*(D & 15) of word D >> 4
+    int* result;          // out: [D, i, j, reason, diagnostics...]
 };
 
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,

@@ -102,241 +102,6 @@ struct PyMT {
     }
 };
 
-}  // namespace
-
-// ------------------------------------------------------------------ context
-struct ga_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    // problem
-    bool loaded = false, custom = false, filled_tb = false;
-    int64_t m = 0, n = 0;      // local problem (slab: n = local columns)
-    int64_t n_global = 0, col0 = 0;
-    int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
-    int nstripes = 0, nslabs = 0, TC = 0;
-    int64_t GV_m = 0, GH_n = 0;
-    std::vector<uint8_t> h_a, h_b;
-    // device buffers
-    DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng,
-        ops, result;
-    DevBuf halo_in{nullptr, 0, true}, prog{nullptr, 0, true};
-    bool slab = false;
-    float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
-    bool dbg_on = false;
-    int ablation = -1;  // diagnostics: fill kernel ablation variant (-1 = product kernel)
-    int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
-    DevBuf dbg;
-};
-
-namespace {
-
-int check_ctx(ga_ctx* c) {
-    if (!c) return fail(GA_E_ARG, "null context");
-    hipError_t e = hipSetDevice(c->device);
-    if (e != hipSuccess) return fail(GA_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
-    return GA_OK;
-}
-
-int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
-                 const int32_t* row0, const int32_t* col0, int64_t cb, int64_t ce) {
-    if (!a || !b_all || !cs || !cs->sub || !cs->gap_h || !cs->gap_v) return fail(GA_E_ARG, "null argument");
-    if (m < 1 || n_all < 1) return fail(GA_E_ARG, "sequences must be non-empty");
-    if (cb < 0 || ce > n_all || ce <= cb) return fail(GA_E_ARG, "bad column slab");
-    const int K = cs->K;
-    if (K < 1 || K > 255) return fail(GA_E_ARG, "alphabet size K must be in [1,255]");
-    if (cs->gap_open < 0) return fail(GA_E_ARG, "gap_open cost must be >= 0");
-    for (int64_t i = 0; i < m; i++)
-        if (a[i] >= K) return fail(GA_E_ARG, "seq_1 code out of range");
-    for (int64_t j = 0; j < n_all; j++)
-        if (b_all[j] >= K) return fail(GA_E_ARG, "seq_2 code out of range");
-    // int32 range guard (DESIGN.md 3): every stored value, shifted or not, and
-    // every intermediate (value + o) must stay far from overflow.
-    int64_t maxabs = 0;
-    for (int q = 0; q < K * K; q++) maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->sub[q]));
-    for (int q = 0; q < K; q++) {
-        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_h[q]));
-        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_v[q]));
-    }
-    const int64_t big = ((int64_t)cs->max_cost + 1) * std::max(m, n_all);
-    int64_t bmax = std::llabs(big);
-    if (row0)
-        for (int64_t q = 0; q < 3 * (n_all + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)row0[q]));
-    if (col0)
-        for (int64_t q = 0; q < 3 * (m + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)col0[q]));
-    const int64_t bound = bmax + (m + n_all + 2) * (3 * maxabs + (int64_t)cs->gap_open);
-    if (4 * bound >= (int64_t)INT32_MAX) return fail(GA_E_RANGE, "problem exceeds the int32 score range of the device path");
-    int64_t subp_max = 0;
-    for (int x = 0; x < K; x++)
-        for (int y = 0; y < K; y++)
-            subp_max = std::max<int64_t>(subp_max,
-                                         std::llabs((long long)cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y]));
-    c->qbytes = subp_max <= 127 ? 1 : subp_max <= 32767 ? 2 : 0;
-    if (!c->qbytes) return fail(GA_E_RANGE, "substitution costs exceed the int16 query profile");
-    const int o = cs->gap_open;
-    c->CB = (o + 1) < 8 ? 1 : (o + 1) < 128 ? 2 : (o + 1) < 32768 ? 4 : 0;
-    if (!c->CB) return fail(GA_E_RANGE, "gap_open cost too large for the traceback word");
-    c->m = m;
-    c->n = ce - cb;
-    c->n_global = n_all;
-    c->col0 = cb;
-    c->K = K;
-    c->o = o;
-    c->big = (int)big;
-    c->custom = row0 != nullptr || col0 != nullptr;
-    if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
-    c->nstripes = (int)((c->n + 63) / 64);
-    c->nslabs = (c->nstripes + ga::NW - 1) / ga::NW;
-    c->h_a.assign(a, a + m);
-    c->h_b.assign(b_all, b_all + n_all);
-    HIPCHK(c->a.ensure(m));
-    HIPCHK(c->b.ensure(n_all));
-    HIPCHK(c->sub.ensure(sizeof(int) * K * K));
-    HIPCHK(c->gh.ensure(sizeof(int) * K));
-    HIPCHK(c->gv.ensure(sizeof(int) * K));
-    HIPCHK(hipMemcpyAsync(c->a.p, a, m, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->b.p, b_all, n_all, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->sub.p, cs->sub, sizeof(int) * K * K, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->gh.p, cs->gap_h, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->gv.p, cs->gap_v, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c->bnd_row.ensure(sizeof(int) * 3 * (n_all + 1)));
-    HIPCHK(c->bnd_col.ensure(sizeof(int) * 3 * (m + 1)));
-    if (c->custom) {
-        HIPCHK(hipMemcpyAsync(c->bnd_row.p, row0, sizeof(int) * 3 * (n_all + 1), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->bnd_col.p, col0, sizeof(int) * 3 * (m + 1), hipMemcpyHostToDevice, c->stream));
-    }
-    {
-        // sub' = sub - gV - gH (DESIGN.md 3), read by the fill's IO wave into its LDS query profile
-        std::vector<int> subp((size_t)K * K);
-        for (int x = 0; x < K; x++)
-            for (int y = 0; y < K; y++) subp[x * K + y] = cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y];
-        HIPCHK(c->qp.ensure(sizeof(int) * K * K));
-        HIPCHK(hipMemcpy(c->qp.p, subp.data(), sizeof(int) * K * K, hipMemcpyHostToDevice));
-        if (ga::fill_lds_bytes(c->CB, c->qbytes, true, K) > 160 * 1024)
-            return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
-    }
-    HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
-    HIPCHK(c->GHp.ensure(sizeof(int) * (n_all + 1)));
-    HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
-    HIPCHK(c->left.ensure(sizeof(int2) * (m + 1)));
-    HIPCHK(c->meta.ensure(sizeof(int) * 8));
-    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
-    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
-    HIPCHK(c->out_last.ensure(sizeof(int) * 4));
-    HIPCHK(c->result.ensure(sizeof(int) * 16));
-    HIPCHK(c->ops.ensure(m + n_all + 1024));  // 2-bit levels; the walk flushes whole 128-byte blocks
-    HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->loaded = true;
-    c->filled_tb = false;
-    return GA_OK;
-}
-
-// Enqueue boundary + query profile + fill.  Does not synchronise.
-int enqueue_fill(ga_ctx* c, int32_t flags) {
-    if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
-    const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
-    const bool full = (flags & GA_FILL_FULL) != 0;
-    const int64_t m = c->m, n = c->n;
-    const int spc = 16 / c->CB;
-    c->TC = (int)((m + 63 + spc - 1) / spc);
-    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->TC * 1024));
-    if (full) {
-        if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
-        HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
-    }
-    unsigned* fl = c->flags.as<unsigned>();
-    // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
-    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
-    ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
-                        c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
-                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom);
-    ga::FillArgs p{};
-    p.a = c->a.as<uint8_t>();
-    p.subp = c->qp.as<int>();
-    p.K = c->K;
-    p.b = c->b.as<uint8_t>() + c->col0;
-    p.top = c->top.as<int2>() + c->col0;
-    if (c->slab && c->col0 > 0) {
-        p.left = c->halo_in.as<int2>();
-        p.left_prog = c->prog.as<unsigned>();  // [0]: halo_in rows
-    } else {
-        p.left = c->left.as<int2>();
-        p.left_prog = nullptr;
-    }
-    p.hand = c->hand.as<int2>();
-    p.hand_prog = fl + 16;
-    p.ticket = fl;
-    p.abort_word = fl + 1;
-    p.tb = tb ? c->tb.as<uint8_t>() : nullptr;
-    p.out_last = c->out_last.as<int>();
-    p.edge_prog = c->slab ? c->prog.as<unsigned>() + 1 : nullptr;  // [1]: halo_out rows
-    p.full = full ? c->full.as<int>() : nullptr;
-    p.m = (int)m;
-    p.n = (int)n;
-    p.o = c->o;
-    p.nstripes = c->nstripes;
-    p.nslabs = c->nslabs;
-    p.TC = c->TC;
-    p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
-    p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
-    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 4 * c->nstripes));
-    p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    if (c->ablation >= 0 && c->CB == 1 && c->qbytes == 1 && !full) ga::launch_fill_ablation(c->stream, p, tb, c->ablation);
-    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    c->filled_tb = tb;
-    return GA_OK;
-}
-
-int finish_fill(ga_ctx* c, int64_t* cost_out, int32_t* full_out) {
-    int last[4] = {0, 0, 0, 0}, meta[2] = {0, 0};
-    unsigned abort_word = 0;
-    HIPCHK(hipMemcpyAsync(last, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(meta, c->meta.p, sizeof(int) * 2, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&abort_word, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipEventElapsedTime(&c->fill_ms, c->ev[0], c->ev[1]));
-    if (abort_word) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
-    c->GV_m = meta[0];
-    // un-shift: cost = H'(m, n) + GV(m) + GH(column)
-    int64_t gh_end = 0;
-    {
-        int v = 0;
-        HIPCHK(hipMemcpy(&v, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost));
-        gh_end = v;
-    }
-    if (cost_out) *cost_out = (int64_t)last[0] + c->GV_m + gh_end;
-    if (full_out) {
-        const int64_t m = c->m, n = c->n, W = n + 1;
-        std::vector<int> GV(m + 1), GH(n + 1);
-        HIPCHK(hipMemcpy(GV.data(), c->GVp.p, sizeof(int) * (m + 1), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(GH.data(), c->GHp.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(full_out, c->full.p, sizeof(int) * 3 * (m + 1) * W, hipMemcpyDeviceToHost));
-        std::vector<int> br(3 * (n + 1)), bc(3 * (m + 1));
-        HIPCHK(hipMemcpy(br.data(), c->bnd_row.p, sizeof(int) * br.size(), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(bc.data(), c->bnd_col.p, sizeof(int) * bc.size(), hipMemcpyDeviceToHost));
-        for (int64_t i = 0; i <= m; i++)
-            for (int64_t j = 0; j <= n; j++) {
-                int* f = full_out + 3 * (i * W + j);
-                if (i == 0) { f[0] = br[3 * j]; f[1] = br[3 * j + 1]; f[2] = br[3 * j + 2]; }
-                else if (j == 0) { f[0] = bc[3 * i]; f[1] = bc[3 * i + 1]; f[2] = bc[3 * i + 2]; }
-                else {
-                    const int sh = GV[i] + GH[j];
-                    f[0] += sh; f[1] += sh; f[2] += sh;
-                }
-            }
-    }
-    return GA_OK;
-}
-
-// Tie-break table for up to `steps` dispatches + MT snapshots every SNAP.
-double now_ms() {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // ---------------------------------------------------------------- tie-break table
 // The dispatcher's 18 draws per step consume a variable number of MT words
 // (getrandbits(2) with rejection: r >= size -> draw again).  The scan below
@@ -485,22 +250,279 @@ void state_after(const RngTable& R, int64_t D, uint32_t* out) {
     out[MTN] = (uint32_t)g.mti;
 }
 
-int run_walk(ga_ctx* c, const std::vector<uint32_t>& tab) {
-    HIPCHK(hipMemcpyAsync(c->rng.p, tab.data(), sizeof(uint32_t) * tab.size(), hipMemcpyHostToDevice, c->stream));
+}  // namespace
+
+// ------------------------------------------------------------------ context
+struct ga_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // problem
+    bool loaded = false, custom = false, filled_tb = false;
+    int64_t m = 0, n = 0;      // local problem (slab: n = local columns)
+    int64_t n_global = 0, col0 = 0;
+    int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
+    int nstripes = 0, nslabs = 0, TC = 0;
+    int64_t GV_m = 0, GH_n = 0;
+    std::vector<uint8_t> h_a, h_b;
+    // device buffers
+    DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng,
+        ops, result;
+    DevBuf halo_in{nullptr, 0, true};
+    bool slab = false;
+    // slab progress words in pinned, coherent host memory: [0] halo_in rows (written by the host
+    // when a band has arrived), [1] halo_out rows (written by the fill's IO wave)
+    uint32_t* prog_host = nullptr;
+    uint32_t* prog_dev = nullptr;
+    int2* halo_in_ext = nullptr;   // caller-bound halo buffers (e.g. tensors RCCL sends from / receives into)
+    int2* halo_out_ext = nullptr;
+    RngTable walk_rng;             // tie-break table of the global problem (slab walks)
+    bool walk_rng_ready = false;
+    float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
+    bool dbg_on = false;
+    int ablation = -1;  // diagnostics: fill kernel ablation variant (-1 = product kernel)
+    int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
+    DevBuf dbg;
+};
+
+namespace {
+
+int check_ctx(ga_ctx* c) {
+    if (!c) return fail(GA_E_ARG, "null context");
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return fail(GA_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    return GA_OK;
+}
+
+int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
+                 const int32_t* row0, const int32_t* col0, int64_t cb, int64_t ce) {
+    if (!a || !b_all || !cs || !cs->sub || !cs->gap_h || !cs->gap_v) return fail(GA_E_ARG, "null argument");
+    if (m < 1 || n_all < 1) return fail(GA_E_ARG, "sequences must be non-empty");
+    if (cb < 0 || ce > n_all || ce <= cb) return fail(GA_E_ARG, "bad column slab");
+    const int K = cs->K;
+    if (K < 1 || K > 255) return fail(GA_E_ARG, "alphabet size K must be in [1,255]");
+    if (cs->gap_open < 0) return fail(GA_E_ARG, "gap_open cost must be >= 0");
+    for (int64_t i = 0; i < m; i++)
+        if (a[i] >= K) return fail(GA_E_ARG, "seq_1 code out of range");
+    for (int64_t j = 0; j < n_all; j++)
+        if (b_all[j] >= K) return fail(GA_E_ARG, "seq_2 code out of range");
+    // int32 range guard (DESIGN.md 3): every stored value, shifted or not, and
+    // every intermediate (value + o) must stay far from overflow.
+    int64_t maxabs = 0;
+    for (int q = 0; q < K * K; q++) maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->sub[q]));
+    for (int q = 0; q < K; q++) {
+        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_h[q]));
+        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_v[q]));
+    }
+    const int64_t big = ((int64_t)cs->max_cost + 1) * std::max(m, n_all);
+    int64_t bmax = std::llabs(big);
+    if (row0)
+        for (int64_t q = 0; q < 3 * (n_all + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)row0[q]));
+    if (col0)
+        for (int64_t q = 0; q < 3 * (m + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)col0[q]));
+    const int64_t bound = bmax + (m + n_all + 2) * (3 * maxabs + (int64_t)cs->gap_open);
+    if (4 * bound >= (int64_t)INT32_MAX) return fail(GA_E_RANGE, "problem exceeds the int32 score range of the device path");
+    int64_t subp_max = 0;
+    for (int x = 0; x < K; x++)
+        for (int y = 0; y < K; y++)
+            subp_max = std::max<int64_t>(subp_max,
+                                         std::llabs((long long)cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y]));
+    c->qbytes = subp_max <= 127 ? 1 : subp_max <= 32767 ? 2 : 0;
+    if (!c->qbytes) return fail(GA_E_RANGE, "substitution costs exceed the int16 query profile");
+    const int o = cs->gap_open;
+    c->CB = (o + 1) < 8 ? 1 : (o + 1) < 128 ? 2 : (o + 1) < 32768 ? 4 : 0;
+    if (!c->CB) return fail(GA_E_RANGE, "gap_open cost too large for the traceback word");
+    c->m = m;
+    c->n = ce - cb;
+    c->n_global = n_all;
+    c->col0 = cb;
+    c->K = K;
+    c->o = o;
+    c->big = (int)big;
+    c->custom = row0 != nullptr || col0 != nullptr;
+    if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
+    c->nstripes = (int)((c->n + 63) / 64);
+    c->nslabs = (c->nstripes + ga::NW - 1) / ga::NW;
+    c->h_a.assign(a, a + m);
+    c->h_b.assign(b_all, b_all + n_all);
+    HIPCHK(c->a.ensure(m));
+    HIPCHK(c->b.ensure(n_all));
+    HIPCHK(c->sub.ensure(sizeof(int) * K * K));
+    HIPCHK(c->gh.ensure(sizeof(int) * K));
+    HIPCHK(c->gv.ensure(sizeof(int) * K));
+    HIPCHK(hipMemcpyAsync(c->a.p, a, m, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->b.p, b_all, n_all, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->sub.p, cs->sub, sizeof(int) * K * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->gh.p, cs->gap_h, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->gv.p, cs->gap_v, sizeof(int) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c->bnd_row.ensure(sizeof(int) * 3 * (n_all + 1)));
+    HIPCHK(c->bnd_col.ensure(sizeof(int) * 3 * (m + 1)));
+    if (c->custom) {
+        HIPCHK(hipMemcpyAsync(c->bnd_row.p, row0, sizeof(int) * 3 * (n_all + 1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->bnd_col.p, col0, sizeof(int) * 3 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    }
+    {
+        // sub' = sub - gV - gH (DESIGN.md 3), read by the fill's IO wave into its LDS query profile
+        std::vector<int> subp((size_t)K * K);
+        for (int x = 0; x < K; x++)
+            for (int y = 0; y < K; y++) subp[x * K + y] = cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y];
+        HIPCHK(c->qp.ensure(sizeof(int) * K * K));
+        HIPCHK(hipMemcpy(c->qp.p, subp.data(), sizeof(int) * K * K, hipMemcpyHostToDevice));
+        if (ga::fill_lds_bytes(c->CB, c->qbytes, true, K) > 160 * 1024)
+            return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
+    }
+    HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
+    HIPCHK(c->GHp.ensure(sizeof(int) * (n_all + 1)));
+    HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
+    HIPCHK(c->left.ensure(sizeof(int2) * (m + 1)));
+    HIPCHK(c->meta.ensure(sizeof(int) * 8));
+    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
+    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
+    HIPCHK(c->out_last.ensure(sizeof(int) * 4));
+    HIPCHK(c->result.ensure(sizeof(int) * 16));
+    HIPCHK(c->ops.ensure(m + n_all + 1024));  // 2-bit levels; the walk flushes whole 128-byte blocks
+    HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->loaded = true;
+    c->filled_tb = false;
+    return GA_OK;
+}
+
+// Enqueue boundary + query profile + fill.  Does not synchronise.
+int enqueue_fill(ga_ctx* c, int32_t flags) {
+    if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
+    const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
+    const bool full = (flags & GA_FILL_FULL) != 0;
+    const int64_t m = c->m, n = c->n;
+    const int spc = 16 / c->CB;
+    c->TC = (int)((m + 63 + spc - 1) / spc);
+    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->TC * 1024));
+    if (full) {
+        if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
+        HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
+    }
+    unsigned* fl = c->flags.as<unsigned>();
+    // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
+    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
+    ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
+                        c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
+                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom);
+    ga::FillArgs p{};
+    p.a = c->a.as<uint8_t>();
+    p.subp = c->qp.as<int>();
+    p.K = c->K;
+    p.b = c->b.as<uint8_t>() + c->col0;
+    p.top = c->top.as<int2>() + c->col0;
+    if (c->slab && c->col0 > 0) {
+        p.left = c->halo_in_ext ? c->halo_in_ext : c->halo_in.as<int2>();
+        p.left_prog = c->prog_dev;  // [0]: halo_in rows
+    } else {
+        p.left = c->left.as<int2>();
+        p.left_prog = nullptr;
+    }
+    p.hand = c->hand.as<int2>();
+    p.hand_prog = fl + 16;
+    p.ticket = fl;
+    p.abort_word = fl + 1;
+    p.tb = tb ? c->tb.as<uint8_t>() : nullptr;
+    p.out_last = c->out_last.as<int>();
+    p.edge_prog = c->slab ? c->prog_dev + 1 : nullptr;  // [1]: halo_out rows
+    p.edge_out = c->slab ? c->halo_out_ext : nullptr;
+    p.full = full ? c->full.as<int>() : nullptr;
+    p.m = (int)m;
+    p.n = (int)n;
+    p.o = c->o;
+    p.nstripes = c->nstripes;
+    p.nslabs = c->nslabs;
+    p.TC = c->TC;
+    p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
+    p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
+    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 4 * c->nstripes));
+    p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    if (c->ablation >= 0 && c->CB == 1 && c->qbytes == 1 && !full) ga::launch_fill_ablation(c->stream, p, tb, c->ablation);
+    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    c->filled_tb = tb;
+    return GA_OK;
+}
+
+int finish_fill(ga_ctx* c, int64_t* cost_out, int32_t* full_out) {
+    int last[4] = {0, 0, 0, 0}, meta[2] = {0, 0};
+    unsigned abort_word = 0;
+    HIPCHK(hipMemcpyAsync(last, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(meta, c->meta.p, sizeof(int) * 2, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&abort_word, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventElapsedTime(&c->fill_ms, c->ev[0], c->ev[1]));
+    if (abort_word) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+    c->GV_m = meta[0];
+    // un-shift: cost = H'(m, n) + GV(m) + GH(column)
+    int64_t gh_end = 0;
+    {
+        int v = 0;
+        HIPCHK(hipMemcpy(&v, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost));
+        gh_end = v;
+    }
+    if (cost_out) *cost_out = (int64_t)last[0] + c->GV_m + gh_end;
+    if (full_out) {
+        const int64_t m = c->m, n = c->n, W = n + 1;
+        std::vector<int> GV(m + 1), GH(n + 1);
+        HIPCHK(hipMemcpy(GV.data(), c->GVp.p, sizeof(int) * (m + 1), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(GH.data(), c->GHp.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(full_out, c->full.p, sizeof(int) * 3 * (m + 1) * W, hipMemcpyDeviceToHost));
+        std::vector<int> br(3 * (n + 1)), bc(3 * (m + 1));
+        HIPCHK(hipMemcpy(br.data(), c->bnd_row.p, sizeof(int) * br.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bc.data(), c->bnd_col.p, sizeof(int) * bc.size(), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i <= m; i++)
+            for (int64_t j = 0; j <= n; j++) {
+                int* f = full_out + 3 * (i * W + j);
+                if (i == 0) { f[0] = br[3 * j]; f[1] = br[3 * j + 1]; f[2] = br[3 * j + 2]; }
+                else if (j == 0) { f[0] = bc[3 * i]; f[1] = bc[3 * i + 1]; f[2] = bc[3 * i + 2]; }
+                else {
+                    const int sh = GV[i] + GH[j];
+                    f[0] += sh; f[1] += sh; f[2] += sh;
+                }
+            }
+    }
+    return GA_OK;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Walk state between slab walks (the C ABI's ga_walk_state without the padding rules).
+struct WalkStart {
+    int64_t i, j, D, h;  // j: global column
+    int L, first;
+};
+
+int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st) {
+    HIPCHK(hipMemcpyAsync(c->rng.p, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, c->stream));
     ga::WalkArgs w{};
     w.tb = c->tb.as<uint8_t>();
     w.CB = c->CB;
     w.TC = c->TC;
     w.a = c->a.as<uint8_t>();
-    w.b = c->b.as<uint8_t>();
-    w.bnd_row = c->bnd_row.as<int>();
+    w.b = c->b.as<uint8_t>() + c->col0;
+    w.bnd_row = c->bnd_row.as<int>() + 3 * c->col0;
     w.bnd_col = c->bnd_col.as<int>();
     w.rng = c->rng.as<uint32_t>();
-    w.nrng = (long long)tab.size();
+    w.nrng = (long long)ntab;
     w.m = (int)c->m;
     w.n = (int)c->n;
     w.o = c->o;
-    w.ops = c->ops.as<uint8_t>();
+    w.i0 = (int)st.i;
+    w.j0 = (int)(st.j - c->col0);
+    w.L0 = st.L;
+    w.first0 = st.first;
+    w.D0 = (int)st.D;
+    w.h0 = (int)st.h;
+    w.handoff = c->col0 > 0;
+    w.maxh = (int)(c->m + c->n_global);
+    w.ops = c->ops.as<uint32_t>();
     w.result = c->result.as<int>();
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     ga::launch_walk(c->stream, w);
@@ -511,10 +533,13 @@ int run_walk(ga_ctx* c, const std::vector<uint32_t>& tab) {
 
 inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 
-int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
-                char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
+// Wait for the walk; decode the levels of dispatches [st.D, D_end) into alignment columns in walk
+// order starting at (st.i, st.j) (global columns).  Returns the end state through `st` and `reason`.
+int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const char* b_chr, char* oa, char* om,
+                 char* ob, int64_t cap, int64_t& len) {
     int res[16];
     HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     c->walk_waits = res[4];
     c->walk_tiles = res[5];
     c->walk_t_tile = res[6];
@@ -523,36 +548,65 @@ int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char
     c->walk_c_total = res[9];
     c->walk_load_ticks = res[10];
     c->walk_load_count = res[11];
-    HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(&c->walk_ms, c->ev[2], c->ev[3]));
-    const int64_t D = res[0];
-    const int reason = res[3];
+    const int64_t D0 = st.D, D1 = res[0];
+    reason = res[3];
     // levels are packed 2 bits per dispatch, dispatch k at bits 30 - 2*(k & 15) of u32 word k >> 4
-    std::vector<uint32_t> ops((D + 15) / 16);
-    if (D) HIPCHK(hipMemcpy(ops.data(), c->ops.p, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    state_after(snaps, D, mt_state);
+    const int64_t w0 = D0 >> 4, w1 = (D1 + 15) >> 4;
+    std::vector<uint32_t> ops((size_t)std::max<int64_t>(w1 - w0, 0));
+    if (D1 > D0)
+        HIPCHK(hipMemcpy(ops.data(), c->ops.as<uint32_t>() + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const int64_t m = c->m, n = c->n_global;
+    int64_t i = st.i, j = st.j;
+    int L = st.L;
+    len = 0;
+    auto put = [&](char x, char y, char z) {
+        if (len < cap) { oa[len] = x; om[len] = y; ob[len] = z; }
+        len++;
+    };
+    if (reason != 4) {
+        for (int64_t k = D0; k < D1; k++) {
+            const char ca = a_chr[pywrap(i - 1, m)], cbb = b_chr[pywrap(j - 1, n)];
+            const unsigned lv = (ops[(k >> 4) - w0] >> (30 - 2 * (k & 15))) & 3u;
+            if (lv == 0) { put(ca, ca == cbb ? '|' : '*', cbb); i--; j--; }
+            else if (lv == 1) { put('-', ' ', cbb); j--; }
+            else { put(ca, ' ', '-'); i--; }
+            L = (int)lv;
+        }
+    }
+    if (D1 > D0) {
+        st.h += (D1 - D0) - (st.first ? 1 : 0);
+        st.first = 0;
+    }
+    st.i = i;
+    st.j = j;
+    st.L = L;
+    st.D = D1;
+    if (len > cap) return fail(GA_E_ARG, "output capacity too small");
+    return GA_OK;
+}
+
+// Whole-problem traceback: one walk from (m, n), tails, reversal (dp_array_backward's output).
+int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
+                char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
+    WalkStart st{c->m, c->n, 0, 0, 0, 1};
+    int reason = 0;
+    int64_t len = 0;
+    if (int r = walk_segment(c, st, reason, a_chr, b_chr, oa, om, ob, cap, len)) return r;
+    state_after(snaps, st.D, mt_state);
     if (reason == 4) {  // IndexError in the reference
         *tb_status = GA_TB_INDEX_ERROR;
         *out_len = 0;
         return GA_OK;
     }
-    const int64_t m = c->m, n = c->n;
-    int64_t i = m, j = n, len = 0;
     auto put = [&](char x, char y, char z) {
         if (len < cap) { oa[len] = x; om[len] = y; ob[len] = z; }
         len++;
     };
-    for (int64_t k = 0; k < D; k++) {
-        const char ca = a_chr[pywrap(i - 1, m)], cbb = b_chr[pywrap(j - 1, n)];
-        const unsigned lv = (ops[k >> 4] >> (30 - 2 * (k & 15))) & 3u;
-        if (lv == 0) { put(ca, ca == cbb ? '|' : '*', cbb); i--; j--; }
-        else if (lv == 1) { put('-', ' ', cbb); j--; }
-        else { put(ca, ' ', '-'); i--; }
-    }
     if (reason == 1)
-        for (int64_t jj = j; jj > 0; jj--) put('-', ' ', b_chr[jj - 1]);
+        for (int64_t jj = st.j; jj > 0; jj--) put('-', ' ', b_chr[jj - 1]);
     else if (reason == 2)
-        for (int64_t ii = i; ii > 0; ii--) put(a_chr[ii - 1], ' ', '-');
+        for (int64_t ii = st.i; ii > 0; ii--) put(a_chr[ii - 1], ' ', '-');
     if (len > cap) return fail(GA_E_ARG, "output capacity too small");
     std::reverse(oa, oa + len);
     std::reverse(om, om + len);
@@ -606,8 +660,9 @@ void ga_ctx_destroy(ga_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
-                      &c->result, &c->halo_in, &c->prog})
+                      &c->result, &c->halo_in})
         b->release();
+    if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -636,7 +691,7 @@ int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
     RngTable R;
     build_rng(mt_state, c->m + c->n + 1, R);
-    if (int r = run_walk(c, R.tab)) return r;
+    if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), WalkStart{c->m, c->n, 0, 0, 0, 1})) return r;
     return finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
 }
 
@@ -652,7 +707,7 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     const double t1 = now_ms();
     build_rng(mt_state, c->m + c->n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
-    if (int r = run_walk(c, R.tab)) return r;
+    if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), WalkStart{c->m, c->n, 0, 0, 0, 1})) return r;
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
     const int rc = finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
@@ -664,33 +719,97 @@ int ga_problem_set_slab(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b
                         int64_t col_begin, int64_t col_end) {
     if (int r = check_ctx(c)) return r;
     c->slab = true;
+    c->halo_in_ext = c->halo_out_ext = nullptr;
+    c->walk_rng_ready = false;
     if (int r = load_problem(c, a, m, b, n, cs, nullptr, nullptr, col_begin, col_end)) return r;
     HIPCHK(c->halo_in.ensure(sizeof(int2) * (m + 1)));
-    HIPCHK(c->prog.ensure(sizeof(unsigned) * 64));
-    HIPCHK(hipMemset(c->prog.p, 0, sizeof(unsigned) * 64));
+    if (!c->prog_host) {
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        c->prog_host = static_cast<uint32_t*>(hp);
+        void* dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, hp, 0));
+        c->prog_dev = static_cast<uint32_t*>(dp);
+    }
+    std::memset(c->prog_host, 0, 256);
+    return GA_OK;
+}
+
+int ga_slab_bind_halos(ga_ctx* c, void* halo_in, void* halo_out) {
+    if (int r = check_ctx(c)) return r;
+    if (!c->slab) return fail(GA_E_STATE, "not a slab context");
+    c->halo_in_ext = static_cast<int2*>(halo_in);
+    c->halo_out_ext = static_cast<int2*>(halo_out);
     return GA_OK;
 }
 
 int ga_slab_buffers(ga_ctx* c, void** halo_in, uint32_t** halo_in_prog, void** halo_out, uint32_t** halo_out_prog) {
     if (int r = check_ctx(c)) return r;
     if (!c->slab) return fail(GA_E_STATE, "not a slab context");
-    if (halo_in) *halo_in = c->halo_in.p;
-    if (halo_in_prog) *halo_in_prog = c->prog.as<uint32_t>();
-    if (halo_out) *halo_out = c->hand.as<int2>() + (size_t)(c->nslabs - 1) * (c->m + 1);
-    if (halo_out_prog) *halo_out_prog = c->prog.as<uint32_t>() + 1;
+    if (halo_in) *halo_in = c->halo_in_ext ? (void*)c->halo_in_ext : c->halo_in.p;
+    if (halo_in_prog) *halo_in_prog = c->prog_host;
+    if (halo_out)
+        *halo_out = c->halo_out_ext ? (void*)c->halo_out_ext
+                                    : (void*)(c->hand.as<int2>() + (size_t)(c->nslabs - 1) * (c->m + 1));
+    if (halo_out_prog) *halo_out_prog = c->prog_host + 1;
     return GA_OK;
 }
 
 int ga_slab_fill_launch(ga_ctx* c, int32_t flags) {
     if (int r = check_ctx(c)) return r;
     if (!c->slab) return fail(GA_E_STATE, "not a slab context");
-    HIPCHK(hipMemsetAsync(c->prog.p, 0, sizeof(unsigned) * 2, c->stream));
+    __atomic_store_n(&c->prog_host[0], 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&c->prog_host[1], 0u, __ATOMIC_SEQ_CST);
     return enqueue_fill(c, flags & GA_FILL_TRACEBACK);
 }
 
 int ga_slab_fill_finish(ga_ctx* c, int64_t* cost_out) {
     if (int r = check_ctx(c)) return r;
     return finish_fill(c, cost_out, nullptr);
+}
+
+int ga_slab_walk_prepare(ga_ctx* c, const uint32_t* mt_state) {
+    if (int r = check_ctx(c)) return r;
+    if (!mt_state) return fail(GA_E_ARG, "null argument");
+    const double t0 = now_ms();
+    build_rng(mt_state, c->m + c->n_global + 1, c->walk_rng);
+    c->rng_ms = (float)(now_ms() - t0);
+    c->walk_rng_ready = true;
+    return GA_OK;
+}
+
+int ga_slab_walk(ga_ctx* c, ga_walk_state* st, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
+                 int64_t cap, int64_t* out_len) {
+    if (int r = check_ctx(c)) return r;
+    if (!st || !a_chr || !b_chr || !oa || !om || !ob || !out_len) return fail(GA_E_ARG, "null argument");
+    if (!c->filled_tb) return fail(GA_E_STATE, "slab walk needs a GA_FILL_TRACEBACK fill first");
+    if (!c->walk_rng_ready) return fail(GA_E_STATE, "call ga_slab_walk_prepare first");
+    *out_len = 0;
+    if (st->reason >= 0 && st->reason != 5) return GA_OK;  // the walk already ended to the right
+    if (st->j != c->col0 + c->n) return fail(GA_E_ARG, "walk state is not at this slab's right edge");
+    if (st->i < 1 || st->i > c->m) return fail(GA_E_ARG, "walk row out of range");
+    WalkStart ws{st->i, st->j, st->D, st->h, st->L, st->first};
+    if (int r = run_walk(c, c->walk_rng.tab.data(), (int64_t)c->walk_rng.tab.size(), ws)) return r;
+    int reason = 0;
+    int64_t len = 0;
+    if (int r = walk_segment(c, ws, reason, a_chr, b_chr, oa, om, ob, cap, len)) return r;
+    st->i = ws.i;
+    st->j = ws.j;
+    st->D = ws.D;
+    st->h = ws.h;
+    st->L = ws.L;
+    st->first = ws.first;
+    st->reason = reason;
+    *out_len = len;
+    return GA_OK;
+}
+
+int ga_slab_mt_state(ga_ctx* c, int64_t D, uint32_t* mt_out) {
+    if (int r = check_ctx(c)) return r;
+    if (!mt_out) return fail(GA_E_ARG, "null argument");
+    if (!c->walk_rng_ready) return fail(GA_E_STATE, "call ga_slab_walk_prepare first");
+    state_after(c->walk_rng, D, mt_out);
+    return GA_OK;
 }
 
 int ga_stream_wait_ge(void* stream, uint32_t* prog, uint32_t value) {

@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
         const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
         const bool src_sc1 = g != 0 || p.left_prog != nullptr;
-        int2* dst = p.hand + (long long)g * (m + 1);
+        int2* dst = (g == p.nslabs - 1 && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
         const int K = p.K;
         unsigned in_next = 0, out_next = 0, spins = 0;
         while (in_next < m || out_next < m) {
@@ -697,7 +697,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     if (wave == 4) {
         // ---------------- helper: tie-break table HBM -> LDS ring, levels LDS ring -> HBM ----------------
         const long long nblk = (w.nrng + 511) / 512;
-        long long rl = 0, fl = 0;
+        long long rl = w.D0 >> 9, fl = w.D0 >> 9;
         for (;;) {
             const int d = sgpr(__hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS));
             const int done = sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS));
@@ -713,7 +713,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
             }
             const long long complete = done ? ((long long)d + 511) / 512 : (d >> 9);
             while (fl < complete) {  // 512 dispatches = 32 words of levels
-                if (lane < 32) reinterpret_cast<uint32_t*>(w.ops)[fl * 32 + lane] = opsbuf[(fl & 3) * 32 + lane];
+                if (lane < 32) w.ops[fl * 32 + lane] = opsbuf[(fl & 3) * 32 + lane];
                 fl++;
                 if (lane == 0) __hip_atomic_store(&ops_flushed, (int)fl, __ATOMIC_RELEASE, WGS);
                 moved = true;
@@ -774,9 +774,10 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     }
 
     // ---------------- walker wave (its loop touches LDS only) ----------------
-    int i = m, j = n, L = 0, D = 0, h = 0, first = 1, reason = -1;
+    int i = w.i0, j = w.j0, L = w.L0, D = w.D0, h = w.h0, first = w.first0, reason = -1;
+    const int jend = w.handoff ? 5 : 2;  // reason when the walk reaches local column 0
     int cti = -1, ctj = -1, nwait = 0, ntiles = 0;
-    const int maxh = m + n;
+    const int maxh = w.maxh;
     unsigned long long t_tile = 0, t_ring = 0;  // time spent waiting (s_memrealtime ticks, 100 MHz)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_start = __builtin_amdgcn_s_memtime();
@@ -816,6 +817,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
 
     // ---- per-step path: the first moves, and degenerate walks, until the walk is in the
     //      interior at a dispatch count that is a multiple of 16 ----
+    if (D & 3) *ops_byte(D) = 0;  // a slab walk may start inside a byte
     for (;;) {
         if (!first && i >= 1 && j >= 1 && (D & 15) == 0) break;
         if ((D & 511) == 0) {
@@ -861,7 +863,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
             continue;
         }
         if (i == 0) { reason = 1; break; }
-        if (j == 0) { reason = 2; break; }
+        if (j == 0) { reason = jend; break; }
         if (++h >= maxh) { reason = 3; break; }
     }
 
@@ -971,7 +973,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                 const int nd = 4 * g + k;
                 opsbuf[(D >> 4) & (RB / 16 - 1)] = ops << (2 * (16 - nd));
                 D += nd;
-                reason = i == 0 ? 1 : 2;
+                reason = i == 0 ? 1 : jend;
                 break;
             }
             opsbuf[(D >> 4) & (RB / 16 - 1)] = ops;

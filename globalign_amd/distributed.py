@@ -1,0 +1,332 @@
+"""Multi-GPU alignment: column slabs, banded edge exchange, walk hand-off.
+
+One process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI on
+ROCm).  seq_2's columns are cut into contiguous slabs, one per rank.  Every
+rank runs its slab's fill as ONE kernel launch; the wavefront crosses a slab
+boundary through a single column of (H', h1') pairs, streamed in row bands:
+
+* rank r's fill publishes its right edge row by row into ``halo_out`` and a
+  progress word in pinned host memory; the host thread sends each band to
+  rank r+1 (``isend``) as soon as the word covers it;
+* rank r+1 posts one ``irecv`` per band into ``halo_in`` and, when a band has
+  landed, raises its own progress word, which the running fill polls.
+
+No device queue ever blocks on a flag (a stream-wait packet could stall an
+RCCL stream sharing its hardware queue), and the only data-path exchange is
+that edge (8 B per row per slab boundary).  Each neighbouring pair gets its
+own 2-rank group so the send and receive directions progress independently.
+
+The traceback walk then runs right to left: the rank owning column n walks
+its slab, hands (i, L, D, h) to its left neighbour, and so on; rank 0
+assembles the columns, appends the reference's tails and reverses
+(dp_array_backward, globaligner.py:395-593, cut at slab edges).
+
+The orchestration only needs an engine exposing the slab interface of
+``_native.Engine`` (load_slab, halo_shape/halo_dtype, slab_bind_halos,
+slab_launch, out_progress, set_in_progress, slab_finish, slab_walk_prepare,
+slab_walk, slab_mt_state); the multi-process CPU tests drive it with a CPU
+engine built on the oracle.
+"""
+import math
+import os
+import time
+
+import numpy as np
+
+
+def slab_bounds(n, world, align=64):
+    """Contiguous column slabs [c_k, c_{k+1}); inner edges on multiples of `align` when n allows."""
+    if world < 1 or n < world:
+        raise ValueError(f"cannot split {n} columns over {world} ranks")
+    edges = [0]
+    for k in range(1, world):
+        e = int(round(n * k / world / align)) * align
+        e = min(max(e, edges[-1] + 1), n - (world - k))
+        edges.append(e)
+    edges.append(n)
+    return edges
+
+
+def bands(m, band):
+    """Row bands (r0, r1), 1-based inclusive, covering rows 1..m."""
+    return [(r0, min(m, r0 + band - 1)) for r0 in range(1, m + 1, band)]
+
+
+class Links:
+    """Process groups of one rank: the pair groups with its neighbours plus a CPU control group."""
+
+    def __init__(self, dist, rank, world):
+        self.rank, self.world = rank, world
+        self.left = self.right = None
+        for k in range(world - 1):
+            g = dist.new_group([k, k + 1])  # every rank takes part in every new_group call
+            if k == rank - 1:
+                self.left = g
+            if k == rank:
+                self.right = g
+        backend = dist.get_backend()
+        self.ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
+        self.device_tensors = backend != "gloo"
+
+
+def stream_edges(dist, links, engine, halo_in, halo_out, m, band, timeout_s=600.0, poll_s=20e-6):
+    """Exchange this rank's slab edges with its neighbours while its fill runs."""
+    import threading
+    rank, world = links.rank, links.world
+    bl = bands(m, band)
+    errors = []
+
+    def receiver(recvs):
+        # gloo's p2p work completes only in wait(); an NCCL work's wait() just orders streams,
+        # so poll its device event instead.  Raise the progress word band by band.
+        try:
+            for k, w in enumerate(recvs):
+                if links.device_tensors:
+                    t0 = time.monotonic()
+                    while not w.is_completed():
+                        if time.monotonic() - t0 > timeout_s:
+                            raise TimeoutError(f"rank {rank}: band {k} never arrived")
+                        time.sleep(poll_s)
+                else:
+                    w.wait()
+                engine.set_in_progress(bl[k][1])
+        except Exception as e:  # surfaced by the caller
+            errors.append(e)
+
+    th = None
+    if rank > 0:
+        recvs = [dist.irecv(halo_in[r0:r1 + 1], src=rank - 1, group=links.left) for (r0, r1) in bl]
+        th = threading.Thread(target=receiver, args=(recvs,), daemon=True)
+        th.start()
+    sends = []
+    if rank < world - 1:
+        t0 = time.monotonic()
+        nsent = 0
+        while nsent < len(bl):
+            prog = engine.out_progress()
+            moved = False
+            while nsent < len(bl) and prog >= bl[nsent][1]:
+                r0, r1 = bl[nsent]
+                sends.append(dist.isend(halo_out[r0:r1 + 1], dst=rank + 1, group=links.right))
+                nsent += 1
+                moved = True
+            if errors:
+                break
+            if not moved:
+                if time.monotonic() - t0 > timeout_s:
+                    raise TimeoutError(f"rank {rank}: right edge stalled at {prog} rows ({nsent}/{len(bl)} bands sent)")
+                time.sleep(poll_s)
+    if th is not None:
+        th.join()
+    if errors:
+        raise errors[0]
+    for w in sends:
+        w.wait()
+
+
+def _send_obj(dist, obj, dst, group):
+    dist.send_object_list([obj], dst=dst, group=group)
+
+
+def _recv_obj(dist, src, group):
+    box = [None]
+    dist.recv_object_list(box, src=src, group=group)
+    return box[0]
+
+
+def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_words, band=4096, torch=None):
+    """Distributed fill + traceback of one problem.  Collective over all ranks.
+
+    Returns (cost, (seq_1_aligned, middle, seq_2_aligned), status, mt_words_after) on rank 0, None elsewhere.
+    status: 0 ok, 1 the reference's IndexError."""
+    rank, world = links.rank, links.world
+    m, n = len(a_codes), len(b_codes)
+    edges = slab_bounds(n, world)
+    c0, c1 = edges[rank], edges[rank + 1]
+    engine.load_slab(a_codes, b_codes, tables, c0, c1)
+    shape, dtype = engine.halo_shape(m), engine.halo_dtype()
+    if links.device_tensors:
+        halo_in = torch.zeros(shape, dtype=dtype, device=engine.torch_device())
+        halo_out = torch.zeros(shape, dtype=dtype, device=engine.torch_device())
+    else:
+        pin = engine.pinned_halos()
+        halo_in = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+        halo_out = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+    engine.slab_bind_halos(halo_in.data_ptr() if rank > 0 else 0, halo_out.data_ptr() if rank < world - 1 else 0,
+                           halo_in, halo_out)
+    engine.slab_launch(traceback=True)
+    engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
+    stream_edges(dist, links, engine, halo_in, halo_out, m, band)
+    cost = engine.slab_finish()
+    ctrl = links.ctrl
+    # ---- walk, right to left
+    if rank == world - 1:
+        state = [m, n, 0, 0, 0, 1, -1]
+    else:
+        state = _recv_obj(dist, rank + 1, ctrl)
+    seg = ("", "", "")
+    if state[6] in (-1, 5):
+        seg, state = engine.slab_walk(state, seq_1, seq_2)
+    if rank > 0:
+        _send_obj(dist, state, rank - 1, ctrl)
+    # ---- assemble on rank 0
+    if world > 1:
+        if rank == world - 1:
+            _send_obj(dist, cost, 0, ctrl)
+        elif rank == 0:
+            cost = _recv_obj(dist, world - 1, ctrl)
+    segs = [None] * world if rank == 0 else None
+    dist.gather_object(seg, segs, dst=0, group=ctrl)
+    if rank != 0:
+        return None
+    i, j, D, reason = state[0], state[1], state[2], state[6]
+    mt_after = engine.slab_mt_state(D)
+    if reason == 4:
+        return cost, ("", "", ""), 1, mt_after
+    parts_a = [s[0] for s in reversed(segs)]
+    parts_m = [s[1] for s in reversed(segs)]
+    parts_b = [s[2] for s in reversed(segs)]
+    sa, sm, sb = "".join(parts_a), "".join(parts_m), "".join(parts_b)
+    if reason == 1:  # walk hit row 0: the rest of seq_2 against gaps
+        tail = seq_2[:j][::-1]
+        sa, sm, sb = sa + "-" * j, sm + " " * j, sb + tail
+    elif reason == 2:
+        tail = seq_1[:i][::-1]
+        sa, sm, sb = sa + tail, sm + " " * i, sb + "-" * i
+    return cost, (sa[::-1], sm[::-1], sb[::-1]), 0, mt_after
+
+
+class GpuSlabEngine:
+    """The product engine (_native.Engine) with the slab interface distributed.py drives."""
+
+    def __init__(self, device):
+        from globalign_amd import _native
+        self.eng = _native.Engine(device)
+        self.device = device
+
+    def load_slab(self, a_codes, b_codes, tables, c0, c1):
+        self.eng.load_slab(a_codes, b_codes, tables, c0, c1)
+
+    def halo_shape(self, m):
+        return (m + 1, 2)
+
+    def halo_dtype(self):
+        import torch
+        return torch.int32
+
+    def torch_device(self):
+        return f"cuda:{self.device}"
+
+    def pinned_halos(self):
+        return True
+
+    def slab_bind_halos(self, in_ptr, out_ptr, halo_in=None, halo_out=None):
+        self.eng.slab_bind_halos(in_ptr, out_ptr)
+
+    def slab_launch(self, traceback=True):
+        self.eng.slab_launch(traceback)
+
+    def out_progress(self):
+        return self.eng.out_progress()
+
+    def set_in_progress(self, rows):
+        self.eng.set_in_progress(rows)
+
+    def slab_finish(self):
+        return self.eng.slab_finish()
+
+    def slab_walk_prepare(self, mt_words):
+        self.eng.slab_walk_prepare(mt_words)
+
+    def slab_walk(self, state, seq_1, seq_2):
+        return self.eng.slab_walk(state, seq_1, seq_2)
+
+    def slab_mt_state(self, D):
+        return self.eng.slab_mt_state(D)
+
+    def timings(self):
+        return self.eng.timings()
+
+
+def init_process_group():
+    """torch.distributed from the torchrun environment (127.0.0.1 rendezvous)."""
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    backend = os.environ.get("GA_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return dist, rank, world, local
+
+
+def bench_main(args, wl, workloads, scoring):
+    """bench.py --gpus N (N > 1): weak scaling of the headline workload.
+
+    Every GPU keeps the per-GPU work of the 1-GPU workload (m*n cells): the
+    matrix grows as a square, side = sqrt(N) * side_1, cut into N column
+    slabs; a step is the whole distributed fill + traceback of one pair."""
+    import torch
+    import bench
+    from globalign_amd import _native
+    dist, rank, world, local = init_process_group()
+    links = Links(dist, rank, world)
+    side = int(round(math.sqrt(world * wl["m"] * wl["n"])))
+    m = n = side
+    s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
+    tables, _ = bench.problem_tables(s1, s2)
+    a_codes, b_codes = tables.codes(s1), tables.codes(s2)
+    import random
+    random.seed(0)
+    mt0 = np.array(random.getstate()[1], dtype=np.uint32)
+    engine = GpuSlabEngine(local if torch.cuda.is_available() else 0)
+    result = None
+
+    def step():
+        return align_slabs(dist, links, engine, s1, s2, a_codes, b_codes, tables, mt0, torch=torch)
+
+    for _ in range(args.warmup):
+        result = step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        result = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX, group=links.ctrl)
+    elapsed = float(el.item())
+    if rank == 0:
+        cost, (sa, _, sb), status, _ = result
+        assert status == 0 and sa.replace("-", "") == s1 and sb.replace("-", "") == s2
+        cells = m * n
+        line = {
+            "metric": bench.METRIC,
+            "value": cells * args.steps / elapsed,
+            "unit": "cells/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (SplitMix64 DNA, SURVEY 8d)",
+            "config": {"workload": f"{wl['desc']}; weak-scaled to {m} x {n} over {world} GPUs "
+                                   f"(column slabs, banded RCCL edge exchange, right-to-left walk hand-off)",
+                       "m": m, "n": n, "traceback": True, "parallelism": f"column slabs x{world}", "cost": cost},
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+import json  # noqa: E402  (used by bench_main)

@@ -92,17 +92,46 @@ int ga_problem_align(ga_ctx* ctx, uint32_t* mt_state, const char* a_chr, const c
  * A context can own the column slab [col_begin, col_end) of a larger problem
  * (global m, n and boundary).  Its left edge arrives in `halo_in`
  * ((m+1) x int2 of (H', h1') in the shifted space of DESIGN.md) guarded by
- * the progress word `halo_in_prog` (rows available); its right edge is
- * produced into ga_slab_halo_out() with progress word ga_slab_halo_out_prog().
- * Both words live in uncached device memory so a stream can wait on / write
- * them (hipStreamWaitValue32 / hipStreamWriteValue32) around RCCL send/recv. */
+ * the progress word `halo_in_prog` (rows available, written by the host when
+ * a band has arrived); its right edge is produced into `halo_out` with the
+ * progress word `halo_out_prog` (rows published by the fill).  Both words are
+ * HOST pointers into pinned coherent memory that the running fill reads and
+ * writes, so the host can stream bands with RCCL send/recv without blocking
+ * a device queue. */
 int ga_problem_set_slab(ga_ctx* ctx, const uint8_t* a, int64_t m, const uint8_t* b, int64_t n, const ga_costs* costs,
                         int64_t col_begin, int64_t col_end);
 int ga_slab_buffers(ga_ctx* ctx, void** halo_in, uint32_t** halo_in_prog, void** halo_out, uint32_t** halo_out_prog);
+/* Use caller-owned device buffers ((m+1) x int2 each) as the slab's left-edge
+ * input and right-edge output (e.g. tensors that RCCL receives into / sends
+ * from); NULL keeps the context's own buffer. */
+int ga_slab_bind_halos(ga_ctx* ctx, void* halo_in, void* halo_out);
 /* Launch the slab fill asynchronously on the context's compute stream. */
 int ga_slab_fill_launch(ga_ctx* ctx, int32_t flags);
 /* Wait for the slab fill; returns H'(m, col_end) un-shifted (only meaningful on the last slab). */
 int ga_slab_fill_finish(ga_ctx* ctx, int64_t* cost_out);
+
+/* Traceback across slabs (dp_array_backward :395-593 cut at slab edges): the
+ * walk starts on the slab owning column n and moves right to left; each slab
+ * continues the state its right neighbour handed over. */
+typedef struct {
+    int64_t i, j;   /* current cell (j: global column)                        */
+    int64_t D, h;   /* dispatches so far; moves after the first one            */
+    int32_t L;      /* level the walk entered the cell with (0 M, 1 X, 2 Y)    */
+    int32_t first;  /* 1 before the first move                                 */
+    int32_t reason; /* -1 running; 0..4 ended (as the whole-problem walk);
+                       5 reached this slab's left edge (continue on the left)  */
+    int32_t pad;
+} ga_walk_state;
+/* Build the host tie-break table of the global problem from the 625-word MT
+ * state (call while the fill runs). */
+int ga_slab_walk_prepare(ga_ctx* ctx, const uint32_t* mt_state);
+/* Walk this slab from *st (j must be the slab's right edge); writes the
+ * alignment columns it produced in walk order (not reversed, no tails) and
+ * updates *st.  a_chr / b_chr: the whole upper-cased sequences. */
+int ga_slab_walk(ga_ctx* ctx, ga_walk_state* st, const char* a_chr, const char* b_chr, char* out_a, char* out_mid,
+                 char* out_b, int64_t cap, int64_t* out_len);
+/* MT state after the first D dispatches (random.getstate()[1] layout). */
+int ga_slab_mt_state(ga_ctx* ctx, int64_t D, uint32_t* mt_state_out);
 /* Enqueue on `stream` (a hipStream_t): wait until *prog >= value / write value to *prog. */
 int ga_stream_wait_ge(void* stream, uint32_t* prog, uint32_t value);
 int ga_stream_write(void* stream, uint32_t* prog, uint32_t value);

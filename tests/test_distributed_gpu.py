@@ -1,0 +1,76 @@
+"""Multi-rank path with the product engine on one MI355X: two ranks on cuda:0 over gloo.
+
+Both ranks' slab fills run concurrently on the same GPU; the left / right
+edges travel through pinned host tensors (the gloo transport), the progress
+words through pinned host memory, exactly as distributed.py drives RCCL on a
+multi-GPU node.  The result must equal the single-problem oracle.
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+from tests.conftest import splitmix_seq
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _scoring(seq_1, seq_2):
+    from globalign_amd.scoring import validate_and_transform_args
+    _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, seq_1[:64], seq_2[:64], match_score=2,
+                                                           mismatch_score=-3, gap_open_score=-5,
+                                                           gap_extension_score=-1)
+    return cmat, goc
+
+
+def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path):
+    import torch
+    import torch.distributed as dist
+    from globalign_amd import distributed
+    from globalign_amd._native import CostTables
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cmat, goc = _scoring(seq_1, seq_2)
+        tables = CostTables(cmat, goc)
+        links = distributed.Links(dist, rank, world)
+        eng = distributed.GpuSlabEngine(0)
+        for _ in range(2):  # the second run reuses the context (buffers, progress words)
+            res = distributed.align_slabs(dist, links, eng, seq_1, seq_2, tables.codes(seq_1),
+                                          tables.codes(seq_2), tables, mt_words, band=band, torch=torch)
+        if rank == 0:
+            cost, strings, status, mt_after = res
+            np.savez(out_path, cost=cost, a=strings[0], mid=strings[1], b=strings[2], status=status,
+                     mt=np.asarray(mt_after, dtype=np.uint32))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,m,n,seed,band", [(2, 3000, 5000, 21, 512), (3, 2100, 4100, 8, 700)])
+def test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path):
+    import torch.multiprocessing as mp
+    from oracle import core
+    seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
+    random.seed(seed)
+    mt_words = np.array(random.getstate()[1], dtype=np.uint32)
+    out = str(tmp_path / "res.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out), nprocs=world,
+                       join=True, start_method="spawn")
+    r = np.load(out)
+    cmat, goc = _scoring(seq_1, seq_2)
+    ref = core.align(seq_1, seq_2, cmat, goc, mt_words)
+    assert int(r["cost"]) == ref["cost"]
+    assert (str(r["a"]), str(r["mid"]), str(r["b"])) == tuple(ref["strings"])
+    assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
