@@ -688,7 +688,8 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     if (threadIdx.x == 0) { load_ticks = 0; load_count = 0; }
     if (threadIdx.x < NSLOT) { tag[threadIdx.x] = -1; busy[threadIdx.x] = 0; }
     if (threadIdx.x < 4) rtag[threadIdx.x] = -1;
-    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = 0; ops_flushed = 0; }
+    // a slab walk starts at dispatch D0: the rings start at its block
+    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; }
     if (CB == 1 && threadIdx.x < 256)
         lut[threadIdx.x] = (uint16_t)cell_shifts(sets_from_code(threadIdx.x & 127u, 1, o), (threadIdx.x >> 7) != 0);
     __syncthreads();
@@ -818,6 +819,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     // ---- per-step path: the first moves, and degenerate walks, until the walk is in the
     //      interior at a dispatch count that is a multiple of 16 ----
     if (D & 3) *ops_byte(D) = 0;  // a slab walk may start inside a byte
+    rng_ready(D);                  // ... and inside a block of entries
     for (;;) {
         if (!first && i >= 1 && j >= 1 && (D & 15) == 0) break;
         if ((D & 511) == 0) {

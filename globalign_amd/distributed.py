@@ -284,7 +284,7 @@ def bench_main(args, wl, workloads, scoring):
     import random
     random.seed(0)
     mt0 = np.array(random.getstate()[1], dtype=np.uint32)
-    engine = GpuSlabEngine(local if torch.cuda.is_available() else 0)
+    engine = GpuSlabEngine(local % max(1, torch.cuda.device_count()))  # ranks may share a GPU (gloo rehearsal)
     result = None
 
     def step():
