@@ -6,13 +6,12 @@
 
 namespace ga {
 
-constexpr int NW = 7;            // compute waves per fill workgroup (+2 IO waves)
-constexpr int RING = 256;        // rows per LDS ring between consecutive waves
-constexpr int TBS = 4;           // traceback staging slots (chunks) per compute wave
-constexpr int QROWS = 1024;      // query-profile ring rows (power of two)
-constexpr int QMASK = QROWS - 1;
+// Row-scan fill: a workgroup = NWC compute waves (4 or 8) + 1 IO wave.
+constexpr int RING = 256;        // rows per LDS edge ring between consecutive waves
 constexpr int RMASK = RING - 1;
+constexpr int FROWS = 16;        // rows per fill chunk (one 16-byte traceback store per lane per CB)
 constexpr int GOUT = 16;         // rows per cross-workgroup publish
+constexpr int FILL_LDS_MIN = 82 * 1024;  // > 80 KB: one fill workgroup per CU
 
 struct FillArgs {
     const uint8_t* a;         // m codes (seq_1)
@@ -31,10 +30,15 @@ struct FillArgs {
     unsigned* edge_prog;      // rows of the right edge published (last slab only; may be null)
     int2* edge_out;           // right edge of the last workgroup slab (nullptr: its hand slot)
     int* full;                // FULL output (shifted M', X', Y') or nullptr
-    int m, n, o, nstripes, nslabs, TC;
+    int m, n, o, nstripes, nslabs, TC;  // TC: 16-byte traceback words per lane per stripe
+    int nwc, qrows;                     // compute waves per workgroup; LDS query-profile ring rows
     unsigned spin_limit, halo_spin_limit;
     unsigned long long* dbg;  // optional timestamps: [nstripes][4] (s_memrealtime) or nullptr
 };
+
+// Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),
+// 16-byte word q holds rows q*SPC+1 .. q*SPC+SPC (SPC = 16/CB), CB bytes per cell:
+//   tb + ((s * TC + q) * 64 + l) * 16 + ((i-1) % SPC) * CB
 
 struct WalkArgs {
     const uint8_t* tb;
@@ -57,8 +61,7 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
                      int o, int big, int* GVp, int* GHp, int2* top, int2* left, int* bnd_row, int* bnd_col, int* meta,
                      bool custom);
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
-size_t fill_lds_bytes(int CB, int qbytes, bool tb, int K);
+size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows);
 void launch_walk(hipStream_t s, const WalkArgs& w);
-void launch_fill_ablation(hipStream_t s, const FillArgs& p, bool tb, int abl);
 
 }  // namespace ga

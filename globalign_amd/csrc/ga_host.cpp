@@ -262,7 +262,7 @@ struct ga_ctx {
     int64_t m = 0, n = 0;      // local problem (slab: n = local columns)
     int64_t n_global = 0, col0 = 0;
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
-    int nstripes = 0, nslabs = 0, TC = 0;
+    int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
     int64_t GV_m = 0, GH_n = 0;
     std::vector<uint8_t> h_a, h_b;
     // device buffers
@@ -280,7 +280,6 @@ struct ga_ctx {
     bool walk_rng_ready = false;
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
     bool dbg_on = false;
-    int ablation = -1;  // diagnostics: fill kernel ablation variant (-1 = product kernel)
     int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
     DevBuf dbg;
 };
@@ -341,8 +340,11 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     c->big = (int)big;
     c->custom = row0 != nullptr || col0 != nullptr;
     if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
+    // one stripe (64 columns) per compute wave; a workgroup (one per CU) chains 4 waves (one per
+    // SIMD: the fastest rows) when every stripe gets a wave that way, else 8 (two per SIMD)
     c->nstripes = (int)((c->n + 63) / 64);
-    c->nslabs = (c->nstripes + ga::NW - 1) / ga::NW;
+    c->nwc = c->nstripes <= 4 * c->num_cu ? 4 : 8;
+    c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
     c->h_a.assign(a, a + m);
     c->h_b.assign(b_all, b_all + n_all);
     HIPCHK(c->a.ensure(m));
@@ -368,7 +370,10 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
             for (int y = 0; y < K; y++) subp[x * K + y] = cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y];
         HIPCHK(c->qp.ensure(sizeof(int) * K * K));
         HIPCHK(hipMemcpy(c->qp.p, subp.data(), sizeof(int) * K * K, hipMemcpyHostToDevice));
-        if (ga::fill_lds_bytes(c->CB, c->qbytes, true, K) > 160 * 1024)
+        // query-profile ring: as many rows as fit 64 KB (at least 128)
+        c->qrows = 1024;
+        while (c->qrows > 128 && (size_t)K * c->qrows * c->qbytes > 64 * 1024) c->qrows >>= 1;
+        if (ga::fill_lds_bytes(c->nwc, c->qbytes, K, c->qrows) > 160 * 1024)
             return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
     }
     HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
@@ -394,8 +399,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
     const bool full = (flags & GA_FILL_FULL) != 0;
     const int64_t m = c->m, n = c->n;
-    const int spc = 16 / c->CB;
-    c->TC = (int)((m + 63 + spc - 1) / spc);
+    // 16-row chunks; CB 16-byte words per lane per chunk (ga_device.h)
+    c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
     if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->TC * 1024));
     if (full) {
         if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
@@ -435,13 +440,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     p.nstripes = c->nstripes;
     p.nslabs = c->nslabs;
     p.TC = c->TC;
+    p.nwc = c->nwc;
+    p.qrows = c->qrows;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 4 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    if (c->ablation >= 0 && c->CB == 1 && c->qbytes == 1 && !full) ga::launch_fill_ablation(c->stream, p, tb, c->ablation);
-    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     c->filled_tb = tb;
@@ -640,6 +646,11 @@ int ga_ctx_create(int device, ga_ctx** out) {
     HIPCHK(hipSetDevice(device));
     ga_ctx* c = new ga_ctx();
     c->device = device;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->num_cu = cus;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(GA_E_HIP, "hipStreamCreate failed");
@@ -853,12 +864,6 @@ int ga_debug_rng(const uint32_t* state, int64_t steps, uint32_t* tab_out, int64_
     if (ms_out) *ms_out = now_ms() - t0;
     std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
     state_after(R, D, state_out);
-    return GA_OK;
-}
-
-int ga_debug_ablation(ga_ctx* c, int abl) {
-    if (!c) return fail(GA_E_ARG, "null context");
-    c->ablation = abl;
     return GA_OK;
 }
 

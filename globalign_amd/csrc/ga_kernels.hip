@@ -17,18 +17,19 @@
 //     H' = min3(M', X', Y')
 // which is exact integer arithmetic (no rounding), so results are bit-exact.
 //
-// Layout (HBM): one wave owns a 64-column stripe; lane l owns column
-// 64*s + l + 1 and processes row t - l + 1 at step t (anti-diagonal skew), so a
-// row's left neighbour is lane l-1's previous step: moved with DPP wave_shr:1.
-// Seven compute waves per workgroup are chained through LDS rings; an eighth
-// (IO) wave moves the slab's left/right edges to/from HBM with write-through
+// Layout (HBM): one wave owns a 64-column stripe and steps down its rows; the
+// horizontal dependence within a row is a prefix-min scan across the lanes
+// (DPP).  NWC compute waves per workgroup are chained through LDS rings; an
+// IO wave moves the slab's left/right edges to/from HBM with write-through
 // (sc1) stores and a progress word (cdna_hip_programming.md Guideline 16, R1).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "ga_device.h"
+#include "ga_row.h"
 
 namespace ga {
 
@@ -37,6 +38,12 @@ namespace ga {
 #define WGS __HIP_MEMORY_SCOPE_WORKGROUP
 
 __device__ __forceinline__ unsigned lds_ld(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, WGS); }
+__device__ __forceinline__ unsigned sgpr_u(unsigned x) { return (unsigned)__builtin_amdgcn_readfirstlane((int)x); }
+// wave-uniform counter read (scalar control flow): LDS executes a wave's operations in
+// order, so a relaxed read of a counter published after its data is enough
+__device__ __forceinline__ unsigned lds_ldu(unsigned* p) {
+    return (unsigned)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(p, __ATOMIC_RELAXED, WGS));
+}
 __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, WGS); }
 __device__ __forceinline__ unsigned g_ld(const unsigned* p) {
     return __hip_atomic_load(const_cast<unsigned*>(p), RLX, AGENT);
@@ -70,7 +77,7 @@ __device__ __forceinline__ bool spin_ok_lds(unsigned& spins, unsigned limit, uns
         __hip_atomic_store(abort_sh, 1u, __ATOMIC_RELAXED, WGS);
         return false;
     }
-    if ((spins & 255u) == 0 && __hip_atomic_load(abort_sh, __ATOMIC_RELAXED, WGS)) return false;
+    if ((spins & 255u) == 0 && lds_ldu(abort_sh)) return false;
     return true;
 }
 
@@ -156,7 +163,19 @@ __global__ void custom_boundary_kernel(const uint8_t* __restrict__ a, int m, con
 }
 
 // ----------------------------------------------------------------------------------
-// The wavefront fill.
+// The row-scan fill (dp_array_forward :366-392, get_next_best_costs :317-363).
+//
+// One wave owns a 64-column stripe; lane l owns column 64s+l+1 and the wave
+// steps down the rows.  Within a row, M' and Y' need only the row above, and
+// the horizontal chain is a prefix minimum:
+//     h1'(i,j) = min(h1'(i,j-1), min(M',Y')(i,j) + o)
+// so with V~ = h1' - o and U = min(M', Y') the whole row's V~ is one inclusive
+// prefix-min scan of U across the 64 lanes (six DPP steps), seeded with the
+// stripe's left edge, and X'(i,j) = V~(i,j-1) + o is a one-lane DPP shift.
+// A wave therefore hands its right edge to the next stripe's wave after a few
+// rows (FROWS-row chunks, published every 4 rows), not after 64 skewed steps:
+// the wavefront ramp across the matrix shrinks from ~nstripes*100 steps to
+// ~nstripes*5 rows.
 //
 // Traceback word of a cell (CB bytes, W = (8*CB-1)/2 bits per field):
 //   bits [0,W)   : min(X - H, o+1)     X in S1 <=> <= o ; M,Y may be in S1 <=> >= o
@@ -166,106 +185,85 @@ __global__ void custom_boundary_kernel(const uint8_t* __restrict__ a, int m, con
 template <int CB>
 struct TbFmt {
     static constexpr int W = (8 * CB - 1) / 2;
-    static constexpr int SPC = 16 / CB;  // steps per 16-byte lane chunk
+    static constexpr int SPC = 16 / CB;  // rows per 16-byte word
 };
 
-struct StepState {
-    int Yc;    // h2' carried from the row above (Y' of this lane's next cell)
-    int HLp;   // H' of the left column one row up (the next cell's diagonal)
-    int Hout;  // this lane's H' of the current row   (to lane l+1)
-    int Xout;  // this lane's h1' of the current row  (to lane l+1)
-};
-
-// BYTES of query profile (one chunk's sub' values for one lane), as raw dwords.
-template <int BYTES>
+// FROWS query-profile values (sub' of one lane's column for 16 rows), raw dwords.
+template <typename QT>
 struct QPack {
-    static constexpr int NWD = (BYTES + 3) / 4;
+    static constexpr int NWD = FROWS * (int)sizeof(QT) / 4;
     uint32_t w[NWD];
-    template <typename T>
-    __device__ static QPack load(const T* p) {
-        QPack r;
-        __builtin_memcpy(r.w, p, sizeof(r.w));
-        return r;
+    __device__ __forceinline__ void load(const QT* p) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int k = 0; k < NWD / 4; k++) {
+            const uint4 v = q[k];
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
     }
-    template <typename QT>
     __device__ __forceinline__ int get(int u) const {
         if (sizeof(QT) == 1) return (int)(int8_t)(w[u >> 2] >> (8 * (u & 3)));
         return (int)(int16_t)(w[u >> 1] >> (16 * (u & 1)));
     }
 };
 
-// ABL: diagnostic ablations (0 in the product): 2 = no DPP (timing only)
-template <int CB, bool MASK, bool FULL, int ABL = 0>
-__device__ __forceinline__ void dp_step(StepState& s, int2 lin, int sub, int o, unsigned op1, int t, int lane, int m,
-                                        bool colok, uint32_t& accw, int sh, int* full, int fullW, int jcol) {
-    constexpr int W = TbFmt<CB>::W;
-    // left neighbour (lane l-1, previous step); lane 0 takes the slab edge from the ring
-    const int HL = (ABL & 2) ? (lin.x ^ s.Hout) : __builtin_amdgcn_update_dpp(lin.x, s.Hout, 0x138, 0xf, 0xf, false);  // wave_shr:1
-    const int XL = (ABL & 2) ? (lin.y ^ s.Xout) : __builtin_amdgcn_update_dpp(lin.y, s.Xout, 0x138, 0xf, 0xf, false);
-    const int Hd = s.HLp;
-    s.HLp = HL;
-    bool act = true;
-    if (MASK) {
-        const int i = t - lane + 1;
-        act = (i >= 1) & (i <= m) & colok;
-    }
-    if (act) {
-        const int M = Hd + sub;
-        const int H = min(min(M, XL), s.Yc);
-        const int Ho = H + o;
-        const unsigned code = min((unsigned)(XL - H), op1) | (min((unsigned)(s.Yc - H), op1) << W) |
-                              (min((unsigned)(M - H), 1u) << (2 * W));
-        if (FULL) {
-            const int i = t - lane + 1;
-            int* f = full + 3 * ((long long)i * fullW + jcol);
-            f[0] = M; f[1] = XL; f[2] = s.Yc;
-        }
-        accw = sh == 0 ? code : (accw | (code << sh));
-        s.Xout = min(XL, Ho);
-        s.Yc = min(s.Yc, Ho);
-        s.Hout = H;
-    } else if (MASK && !colok) {
-        s.Hout = HL;  // columns beyond n forward their left input unchanged
-        s.Xout = XL;
-    }
+// one step of an inclusive prefix-min scan over the wave (DPP; disabled lanes keep INT_MAX)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_min(int x) {
+    return min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, CTRL, ROWMASK, 0xf, false));
+}
+__device__ __forceinline__ int wave_scan_min(int x) {
+    x = dpp_min<0x111, 0xf>(x);  // row_shr:1
+    x = dpp_min<0x112, 0xf>(x);  // row_shr:2
+    x = dpp_min<0x114, 0xf>(x);  // row_shr:4
+    x = dpp_min<0x118, 0xf>(x);  // row_shr:8
+    x = dpp_min<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+    x = dpp_min<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// lane l takes lane l-1's value; lane 0 takes `edge`
+__device__ __forceinline__ int shr1(int edge, int x) { return __builtin_amdgcn_update_dpp(edge, x, 0x138, 0xf, 0xf, false); }
+
+// LDS byte address of a __shared__ object (for hand-issued ds_read)
+template <typename T>
+__device__ __forceinline__ unsigned lds_addr(T* p) {
+    return (unsigned)(uintptr_t)(__attribute__((address_space(3))) T*)p;
+}
+// single-lane LDS stores with a narrowed exec mask (no branch: the compute loop keeps
+// scalar control flow; a structured `if (lane == k)` turns uniform values into VGPR phis)
+typedef int v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_store_lane0(unsigned addr, unsigned v) {
+    unsigned long long saved;
+    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\tds_write_b32 %1, %2\n\ts_mov_b64 exec, %0"
+                 : "=&s"(saved) : "v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_store2_b128_lane(unsigned addr, unsigned long long lanemask, v4i a, v4i b) {
+    unsigned long long saved;
+    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %2\n\tds_write_b128 %1, %3\n\tds_write_b128 %1, %4 offset:16\n\ts_mov_b64 exec, %0"
+                 : "=&s"(saved) : "v"(addr), "s"(lanemask), "v"(a), "v"(b) : "memory");
 }
 
 
+// LDS: counters | ring[NWC+1][RING] (int2) | qring[K][qrows] (QT)
+//   ring k feeds compute wave k (ring 0 from the IO wave, ring k+1 from wave k; the IO
+//   wave drains ring nlive).  Slot (i-1) & RMASK of a ring holds what row i of the
+//   next stripe needs from its left edge: (H'(i-1, edge), V~(i, edge)) with
+//   V~ = h1' - o, one broadcast 8-byte read per row.
+//   prod[k] = P: slots of rows <= P are written (the H' of row P itself lands with row P+1);
+//   cons[k] = C: the reader of ring k no longer needs slots < C;
+//   prodq = Q: query-profile rows <= Q are written (the IO wave runs it ahead of the edges).
+enum { CI_PROD = 0, CI_CONS = 16, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
+constexpr int FILL_CNT_BYTES = 256;
 
-// ABL (diagnostic ablations, 0 in the product): 1 = no ring write, 2 = no DPP, 4 = no ring
-// read, 8 = no query-profile reads, 16 = no inter-wave waits.
-//
-// Workgroup = NW compute waves + 2 IO waves, all communication through LDS.
-// Compute waves issue no HBM operation at all (their steady loop is VALU + LDS):
-//   * IO-A (wave NW) moves the slab's left edge in (HBM -> ring 0), the right edge
-//     out (ring NW -> HBM, write-through + progress word) and fills the query
-//     profile ring qring[code][row] from seq_1 (sub' = sub - gV - gH);
-//   * IO-B (wave NW+1) streams the compute waves' traceback words from LDS
-//     staging slots to HBM.
-// LDS layout (dynamic, byte offsets from FillLds::*).
-struct FillLds {
-    static constexpr int CNT = 0;                                  // u32 counters (see CI_*)
-    static constexpr int RINGS = 256;                              // (NW+1) x RING x int2
-    static constexpr int DUMMY = RINGS + (NW + 1) * RING * 8;      // 64 x 17 x int2 sink for lanes 0..62
-    static constexpr int TBST = DUMMY + 64 * 17 * 8;               // NW x TBS x 64 x 16 B
-    static constexpr int QRING_TB = TBST + NW * TBS * 1024;
-    static constexpr int QRING_NOTB = TBST;
-};
-enum { CI_PROD = 0, CI_CONS = 8, CI_TBPROD = 16, CI_TBCONS = 24, CI_ABORT = 32, CI_SLAB = 33 };
-
-template <int CB, typename QT, bool TB, bool FULL, int ABL = 0>
-__global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
-    constexpr int SPC = TbFmt<CB>::SPC;
+template <int CB, typename QT, bool TB, bool FULL, int NWC>
+__global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
+    constexpr int W = TbFmt<CB>::W;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    unsigned* cnt = reinterpret_cast<unsigned*>(smem + FillLds::CNT);
-    int2* rings = reinterpret_cast<int2*>(smem + FillLds::RINGS);
-    int2* dummy = reinterpret_cast<int2*>(smem + FillLds::DUMMY);
-    uint4* tbst = reinterpret_cast<uint4*>(smem + FillLds::TBST);
-    QT* qring = reinterpret_cast<QT*>(smem + (TB ? FillLds::QRING_TB : FillLds::QRING_NOTB));
+    unsigned* cnt = reinterpret_cast<unsigned*>(smem);
+    int2* ring = reinterpret_cast<int2*>(smem + FILL_CNT_BYTES);
+    QT* qring = reinterpret_cast<QT*>(ring + (NWC + 1) * RING);
     unsigned* prod = cnt + CI_PROD;
     unsigned* cons = cnt + CI_CONS;
-    unsigned* tbprod = cnt + CI_TBPROD;
-    unsigned* tbcons = cnt + CI_TBCONS;
     unsigned* abort_sh = cnt + CI_ABORT;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave index: uniform
@@ -273,59 +271,82 @@ __global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
     __syncthreads();
     if (threadIdx.x == 0) cnt[CI_SLAB] = atomicAdd(p.ticket, 1u);
     __syncthreads();
-    const int g = __builtin_amdgcn_readfirstlane((int)cnt[CI_SLAB]);  // uniform: scalar branches below
-    const unsigned m = (unsigned)p.m;
-    const int QSTRIDE = QROWS + SPC;  // per code: QROWS slots + SPC mirrored rows (no wrap inside a chunk)
-    const int T = (int)m + 63;
-    const int nchunks = (T + SPC - 1) / SPC;
+    const int g = __builtin_amdgcn_readfirstlane((int)cnt[CI_SLAB]);  // slab of this workgroup (ticket order)
+    const int m = p.m, o = p.o;
+    const int nch = (m + FROWS - 1) / FROWS;
+    const int mpad = nch * FROWS;
+    const int nlive = min(NWC, p.nstripes - g * NWC);
+    const int QR = p.qrows;
+    const unsigned qmask = (unsigned)QR - 1u;
 
-    if (w == NW) {
-        // ---------------- IO-A: slab edges HBM <-> LDS rings, query profile ----------------
+    if (w == NWC) {
+        // ---------------- IO wave: slab edges HBM <-> LDS rings, query profile ----------------
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
         const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
         const bool src_sc1 = g != 0 || p.left_prog != nullptr;
-        int2* dst = (g == p.nslabs - 1 && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
+        const bool last_slab = g == p.nslabs - 1;
+        int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
+        int2* rin0 = ring;
+        const int2* rout = ring + nlive * RING;
         const int K = p.K;
-        unsigned in_next = 0, out_next = 0, spins = 0;
-        while (in_next < m || out_next < m) {
+        const int h00 = p.top[g * NWC * 64].x;  // H'(0, left edge)
+        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
+        while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
-            if (in_next < m) {
-                // ring 0 slots are reused after wave 0 read them; query-profile rows after
-                // the last compute wave's lanes all passed them (its output count)
-                const unsigned space = min(lds_ld(&cons[0]) + RING, lds_ld(&prod[NW]) + QROWS - 2 * SPC);
-                const unsigned avail = src_prog ? min(g_ld(src_prog), m) : m;
+            if (q_next < (unsigned)m) {
+                // profile rows of chunks the slowest wave (ring nlive's producer) has finished are free
+                const unsigned pl = lds_ld(&prod[nlive]);
+                const unsigned space = (pl & ~(unsigned)(FROWS - 1)) + QR - FROWS;
+                const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
+                if (hi > q_next) {
+                    const unsigned r = q_next + 1 + lane;
+                    if (r <= hi) {
+                        const int x = p.a[r - 1];
+                        const int* sp = p.subp + x * K;
+                        QT* qd = qring + ((r - 1) & qmask);
+                        for (int c = 0; c < K; c++) qd[c * QR] = (QT)sp[c];
+                    }
+                    if (lane == 0) lds_st(&cnt[CI_PRODQ], hi == (unsigned)m ? (unsigned)mpad : hi);
+                    q_next = hi;
+                    moved = true;
+                }
+            }
+            if (in_next < (unsigned)m) {
+                // ring 0 slots are free below cons[0]
+                const unsigned space = lds_ld(&cons[0]) + RING;
+                const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
                     const unsigned r = in_next + 1 + lane;
                     if (r <= hi) {
-                        rings[(r + 62) & RMASK] = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
-                        const int x = p.a[r - 1];
-                        const int slot = r & QMASK;
-                        const int* sp = p.subp + x * K;
-                        for (int c = 0; c < K; c++) {
-                            const QT v = (QT)sp[c];
-                            qring[c * QSTRIDE + slot] = v;
-                            if (slot < SPC) qring[c * QSTRIDE + QROWS + slot] = v;
-                        }
+                        const int2 e1 = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
+                        const int h0 = r == 1 ? h00 : (src_sc1 ? unpack64(g_ld64(src + r - 1)) : src[r - 1]).x;
+                        rin0[(r - 1) & RMASK] = make_int2(h0, e1.y - o);
                     }
-                    if (lane == 0) lds_st(&prod[0], hi);
+                    // rows past m are padding (garbage nobody reads back)
+                    if (lane == 0) lds_st(&prod[0], hi == (unsigned)m ? (unsigned)mpad : hi);
                     in_next = hi;
                     moved = true;
                 }
             }
-            if (out_next < m) {
-                const unsigned avail = lds_ld(&prod[NW]);
-                const unsigned hi = min(avail, out_next + 64);
-                if (hi > out_next && (hi - out_next >= GOUT || hi == m)) {
+            if (out_next < (unsigned)m) {
+                // row r of the right edge: H' from slot r (row r+1's entry), V~ from slot r-1
+                const unsigned P = lds_ld(&prod[nlive]);
+                const unsigned hi = min(min(P, (unsigned)mpad + 1u) - 1u, min((unsigned)m, out_next + 64));
+                if (P > 0 && hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
                     const unsigned r = out_next + 1 + lane;
-                    if (r <= hi) g_st64(dst + r, rings[NW * RING + ((r + 62) & RMASK)]);
+                    if (r <= hi) {
+                        const int H = rout[r & RMASK].x;
+                        g_st64(dst + r, make_int2(H, rout[(r - 1) & RMASK].y + o));
+                        if (last_slab && r == (unsigned)m) p.out_last[0] = H;  // H'(m, n): the cost
+                    }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) {
                         g_st(p.hand_prog + g, hi);
-                        if (p.edge_prog != nullptr && g == p.nslabs - 1)
+                        if (p.edge_prog != nullptr && last_slab)
                             __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
-                        lds_st(&cons[NW], hi);
+                        lds_st(&cons[nlive], hi - 1u);
                     }
                     out_next = hi;
                     moved = true;
@@ -346,144 +367,184 @@ __global__ void __launch_bounds__(64 * (NW + 2)) fill_kernel(FillArgs p) {
         }
         return;
     }
-
-    if (w == NW + 1) {
-        // ---------------- IO-B: traceback words LDS staging -> HBM ----------------
-        if (!TB) return;
-        unsigned done[NW];
-        int nlive = 0;
-#pragma unroll
-        for (int k = 0; k < NW; k++) {
-            done[k] = 0;
-            nlive += (g * NW + k) < p.nstripes;
-        }
-        unsigned spins = 0;
-        for (;;) {
-            bool moved = false, all = true;
-#pragma unroll
-            for (int k = 0; k < NW; k++) {
-                if (k >= nlive) continue;
-                const unsigned avail = lds_ld(&tbprod[k]);
-                if (avail > done[k]) {
-                    const long long s = (long long)g * NW + k;
-                    uint4* dstp = reinterpret_cast<uint4*>(p.tb) + (s * p.TC) * 64 + lane;
-                    for (unsigned cc = done[k]; cc < avail; cc++)
-                        dstp[(long long)cc * 64] = tbst[(k * TBS + (cc % TBS)) * 64 + lane];
-                    done[k] = avail;
-                    if (lane == 0) lds_st(&tbcons[k], avail);  // the LDS reads above are complete
-                    moved = true;
-                }
-                all &= done[k] >= (unsigned)nchunks;
-            }
-            if (all) break;
-            if (!moved) {
-                if (__hip_atomic_load(abort_sh, RLX, WGS)) break;
-                if (!spin_ok(spins, p.spin_limit, p.abort_word)) {
-                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
-                    break;
-                }
-            } else {
-                spins = 0;
-            }
-        }
-        return;
-    }
+    if (w >= nlive) return;
 
     // ---------------- compute wave w: stripe s ----------------
-    const int s = g * NW + w;
-    const bool live = s < p.nstripes;
-    const int jcol = s * 64 + lane + 1;               // 1-based column of this lane
-    const bool colok = live && jcol <= p.n;
-    const bool full_stripe = live && (s * 64 + 64 <= p.n);
+    const int s = g * NWC + w;
+    const int j0 = s * 64;                    // columns j0+1 .. j0+64
+    const int jcol = j0 + lane + 1;
+    const bool colok = jcol <= p.n;
+    const int srcl = min(63, p.n - 1 - j0);   // the lane whose column is this stripe's right edge
     const int bcode = colok ? p.b[jcol - 1] : 0;
-    const QT* qcol = qring + bcode * QSTRIDE;
-    StepState st;
+    const QT* qcol = qring + bcode * QR;
+    int Hprev, Yc;                            // H'(i-1, j), h2'(i-1, j)
     {
-        const int jt = colok ? jcol : 0;
-        st.Hout = p.top[jt].x;                       // H'(0, j)
-        st.Yc = p.top[jt].y;                         // h2'(0, j)
-        st.HLp = p.top[colok ? jcol - 1 : 0].x;      // H'(0, j-1): diagonal of row 1
-        st.Xout = 0;
+        const int2 t = p.top[colok ? jcol : p.n];
+        Hprev = t.x;
+        Yc = t.y;
     }
-    const int o = p.o;
     const unsigned op1 = (unsigned)o + 1u;
-    const int2* rin = rings + w * RING;
-    // lanes 0..62 write into their own sink rows, 17 int2 apart: the per-lane stride of 34
-    // dwords spreads a 16-lane ds_write_b64 group over all 32 banks (no conflicts)
-    int2* const aout = lane == 63 ? rings + (w + 1) * RING : dummy + lane * 17;
-    const unsigned aout_mask = lane == 63 ? (unsigned)RMASK : 0u;
-    unsigned spins = 0, avail = 0, outfree = RING, tbfree = TBS;
-    unsigned long long stamp0 = 0, stamp1 = 0;
-    bool ok = true;
+    const int2* rin = ring + w * RING;
+    int2* rout = ring + (w + 1) * RING;
+    uint4* tbw = TB ? reinterpret_cast<uint4*>(p.tb) + (long long)s * p.TC * 64 + lane : nullptr;
+    unsigned avail = 0, outfree = 0, qavail = 0;
+    unsigned long long stamp0 = 0, stamp1 = 0, clk0 = 0;
+    const unsigned prod_out_lds = lds_addr(&prod[w + 1]);
+    const unsigned cons_lds = lds_addr(&cons[w]);
+    const unsigned rout_lds = lds_addr(rout);
+    const unsigned long long srcmask = 1ull << srcl;
+    // wait (wave-uniform) until *ctr + add >= target.  A wait that gives up (the workgroup
+    // aborted) makes every later wait a no-op: the wave runs to its end on garbage and the
+    // host reports the abort word, so the loops below have no early exits (clean unrolling).
+    bool aborted = false;
+    auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target) {
+        unsigned spins = 0;
+        cached = sgpr_u(cached);
+        while ((int)cached < target && !aborted) {
+            cached = lds_ldu(ctr) + add;
+            if ((int)cached >= target) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) aborted = true;
+        }
+        // the reads of what the counter guards stay after it (the LDS itself keeps order)
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    };
+    wait_ge(&prod[w], 0, avail, 4);  // rows 1..4 before the first edge read
+    int4 e01 = reinterpret_cast<const int4*>(rin)[0];  // slots 0..3: (H'(i-1), V~(i)) of rows 1..4
+    int4 e23 = reinterpret_cast<const int4*>(rin)[1];
+    // the counter is read one sub-chunk before it is needed (a plain load: the asm stores'
+    // memory clobbers keep the compiler from reusing an old value, and it waits at the use)
+    const unsigned* prod_in = &prod[w];
+    unsigned pnext = *prod_in;
 
-    for (int c = 0; c < nchunks && ok; c++) {
-        const int t0 = c * SPC;
-        if (p.dbg != nullptr && c == 1) stamp0 = __builtin_amdgcn_s_memrealtime();
-        if (p.dbg != nullptr && c == nchunks / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
-        // inputs: rows t0+1 .. t0+SPC in ring w (counter read only when needed)
-        const unsigned need = min((unsigned)(t0 + SPC), m);
-        while (!(ABL & 16) && avail < need) {
-            avail = lds_ld(&prod[w]);
-            if (avail >= need) break;
-            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
-        }
-        // outputs: rows t0-62 .. t0+SPC-63; a ring slot is reused RING rows later
-        const int hi_out = t0 + SPC - 63;
-        while (!(ABL & 16) && (int)outfree < hi_out) {
-            outfree = lds_ld(&cons[w + 1]) + RING;
-            if ((int)outfree >= hi_out) break;
-            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
-        }
-        // traceback staging slot c % TBS must have been drained (chunk c - TBS)
-        while (TB && live && !(ABL & 16) && tbfree < (unsigned)c + 1u) {
-            tbfree = lds_ld(&tbcons[w]) + TBS;
-            if (tbfree >= (unsigned)c + 1u) break;
-            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) { ok = false; break; }
-        }
-        if (!ok) break;
-        spins = 0;
-        if (lane == 0) __hip_atomic_store(&cons[w], min((unsigned)t0, m), RLX, WGS);
-        // this chunk's left-edge rows (broadcast) and substitution values (per lane)
-        int2 lin[SPC];
-        int qv[SPC];
-        const QT* qa = qcol + ((t0 + 1 - lane) & QMASK);
+    // traceback codes are software-pipelined one sub-chunk behind the DP chain, so their
+    // VALU work fills the chain's DPP hazard slots: pM/pX/pY/pH hold the previous
+    // sub-chunk's rows, accP the previous chunk's words (finished in sub-chunk 0)
+    int pM[4] = {0, 0, 0, 0}, pX[4] = {0, 0, 0, 0}, pY[4] = {0, 0, 0, 0}, pH[4] = {0, 0, 0, 0};
+    uint32_t accP[4 * CB];
 #pragma unroll
-        for (int u = 0; u < SPC; u++) {
-            lin[u] = (ABL & 4) ? make_int2(t0 + u, u) : rin[(t0 + 63 + u) & RMASK];
-            qv[u] = (ABL & 8) ? (u - 3) : (int)qa[u];
-        }
-        int2* ao = aout + ((unsigned)t0 & aout_mask);
-        uint32_t acc[4] = {0, 0, 0, 0};
-        const bool steady = full_stripe && t0 >= 63 && t0 + SPC - 1 <= (int)m - 1;
-        if (steady) {
+    for (int k = 0; k < 4 * CB; k++) accP[k] = 0;
+    auto code_of = [&](int u) -> unsigned {
+        return min((unsigned)(pX[u] - pH[u]), op1) | (min((unsigned)(pY[u] - pH[u]), op1) << W) |
+               (min((unsigned)(pM[u] - pH[u]), 1u) << (2 * W));
+    };
+    auto store_words = [&](int cc, const uint32_t* wds) {
 #pragma unroll
-            for (int u = 0; u < SPC; u++) {
-                dp_step<CB, false, FULL, ABL>(st, lin[u], qv[u], o, op1, t0 + u, lane, m, true, acc[(u * CB) >> 2],
-                                              (u * CB * 8) & 31, p.full, p.n + 1, jcol);
-                if (!(ABL & 1)) ao[u] = make_int2(st.Hout, st.Xout);
+        for (int k = 0; k < CB; k++)
+            tbw[(long long)(cc * CB + k) * 64] = make_uint4(wds[4 * k], wds[4 * k + 1], wds[4 * k + 2], wds[4 * k + 3]);
+    };
+
+    for (int c = 0; c < nch; c++) {
+        const int row0 = __builtin_amdgcn_readfirstlane(c * FROWS);
+        if (p.dbg != nullptr && c == 1) {
+            stamp0 = __builtin_amdgcn_s_memrealtime();
+            clk0 = __builtin_amdgcn_s_memtime();
+        }
+        if (p.dbg != nullptr && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
+        // output ring slots row0 .. row0+FROWS (the tail write included) must be free
+        wait_ge(&cons[w + 1], RING, outfree, row0 + FROWS + 1);
+        wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + FROWS);
+        QPack<QT> q;
+        q.load(qcol + ((unsigned)row0 & qmask));
+        uint32_t acc[4 * CB];
+#pragma unroll
+        for (int k = 0; k < 4 * CB; k++) acc[k] = 0;
+#pragma unroll
+        for (int sc = 0; sc < FROWS / 4; sc++) {
+            const int r0 = __builtin_amdgcn_readfirstlane(row0 + 4 * sc);  // rows r0+1 .. r0+4 (edges in e01/e23)
+            const int eh[4] = {e01.x, e01.z, e23.x, e23.z};  // H'(i-1, edge)
+            const int ev[4] = {e01.y, e01.w, e23.y, e23.w};  // V~(i, edge)
+            int4 n01, n23;                    // the next sub-chunk's edges
+            int sM[4], sX[4], sY[4], sH[4], oH[4], oV[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int uu = 4 * sc + u;       // row within the chunk; row i = row0 + uu + 1
+                int M, X, H, Vt, Ycn;
+                if (TB && !FULL) {
+                    // the code of row u of the previous sub-chunk (of the previous chunk when sc == 0)
+                    constexpr int QB = (int)sizeof(QT);
+                    const int pu = (4 * ((sc + 3) & 3) + u) * CB;
+                    uint32_t& dstw = sc == 0 ? accP[pu >> 2] : acc[pu >> 2];
+                    const uint32_t qw = q.w[(uu * QB) >> 2];
+                    const unsigned sh = (unsigned)(pu * 8 & 31);
+                    switch (((uu * QB) & 3) / QB) {
+                        case 0: row_asm<W, 0, QB == 2>(Hprev, Yc, eh[u], ev[u], qw, pM[u], pX[u], pY[u], pH[u], op1, o, sh, dstw, M, X, H, Vt, Ycn); break;
+                        case 1: row_asm<W, 1, QB == 2>(Hprev, Yc, eh[u], ev[u], qw, pM[u], pX[u], pY[u], pH[u], op1, o, sh, dstw, M, X, H, Vt, Ycn); break;
+                        case 2: row_asm<W, 2, QB == 2>(Hprev, Yc, eh[u], ev[u], qw, pM[u], pX[u], pY[u], pH[u], op1, o, sh, dstw, M, X, H, Vt, Ycn); break;
+                        default: row_asm<W, 3, QB == 2>(Hprev, Yc, eh[u], ev[u], qw, pM[u], pX[u], pY[u], pH[u], op1, o, sh, dstw, M, X, H, Vt, Ycn); break;
+                    }
+                } else {
+                    M = shr1(eh[u], Hprev) + q.get(uu);
+                    Vt = min(wave_scan_min(min(M, Yc)), ev[u]);
+                    X = shr1(ev[u], Vt) + o;
+                    H = min(min(M, X), Yc);
+                    Ycn = min(Yc, H + o);
+                    if (TB) {
+                        const int pu = (4 * ((sc + 3) & 3) + u) * CB;
+                        uint32_t* dstw = sc == 0 ? accP : acc;
+                        dstw[pu >> 2] |= code_of(u) << (pu * 8 & 31);
+                    }
+                }
+                if (FULL) {
+                    const int i = row0 + uu + 1;
+                    if (colok && i <= m) {
+                        int* f = p.full + 3 * ((long long)i * (p.n + 1) + jcol);
+                        f[0] = M; f[1] = X; f[2] = Yc;
+                    }
+                }
+                if (u == 0) {
+                    // after one row (the previous sub-chunk's ring writes have landed): check the
+                    // next sub-chunk's rows and read their edges, three rows before their use
+                    if (r0 + 4 < mpad) {
+                        avail = sgpr_u(max(avail, pnext));
+                        wait_ge(&prod[w], 0, avail, r0 + 8);
+                    }
+                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 4) & RMASK));
+                    n01 = e4[0];
+                    n23 = e4[1];
+                    pnext = *prod_in;
+                }
+                sM[u] = M; sX[u] = X; sY[u] = Yc; sH[u] = H;
+                oH[u] = Hprev;
+                oV[u] = Vt;
+                Yc = Ycn;
+                Hprev = H;
             }
-        } else {
 #pragma unroll
-            for (int u = 0; u < SPC; u++) {
-                dp_step<CB, true, FULL, ABL>(st, lin[u], qv[u], o, op1, t0 + u, lane, m, colok, acc[(u * CB) >> 2],
-                                             (u * CB * 8) & 31, p.full, p.n + 1, jcol);
-                if (!(ABL & 1)) ao[u] = make_int2(st.Hout, st.Xout);
+            for (int u = 0; u < 4; u++) { pM[u] = sM[u]; pX[u] = sX[u]; pY[u] = sY[u]; pH[u] = sH[u]; }
+            if (TB && sc == 0) {
+                // the previous chunk's words are complete
+                if (c > 0) store_words(c - 1, accP);
             }
+            // the right edge of these rows goes out; LDS executes one wave's operations in
+            // order: the rows land before the counters
+            lds_store2_b128_lane(rout_lds + (unsigned)(r0 & RMASK) * 8u, srcmask, v4i{oH[0], oV[0], oH[1], oV[1]},
+                                 v4i{oH[2], oV[2], oH[3], oV[3]});
+            lds_store_lane0(prod_out_lds, (unsigned)(r0 + 4));
+            lds_store_lane0(cons_lds, (unsigned)(r0 + 3));
+            e01 = n01;
+            e23 = n23;
         }
-        if (TB && live) tbst[(w * TBS + (c % TBS)) * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-        if (lane == 0) {
-            // one release (lgkmcnt(0)) covers the ring rows and the staged words
-            if (TB && live) lds_st(&tbprod[w], (unsigned)c + 1u);
-            if (hi_out >= 1) lds_st(&prod[w + 1], min((unsigned)hi_out, m));
-        }
+#pragma unroll
+        for (int k = 0; k < 4 * CB; k++) accP[k] = acc[k];
     }
-    if (p.dbg != nullptr && lane == 0 && live) {
+    if (TB) {
+        // the last sub-chunk's codes, then the last chunk's words
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int pu = (12 + u) * CB;
+            accP[pu >> 2] |= code_of(u) << (pu * 8 & 31);
+        }
+        store_words(nch - 1, accP);
+    }
+    // H' of the last (padded) row, for the reader's hand-off of row m when m == mpad
+    if (lane == srcl) rout[mpad & RMASK].x = Hprev;
+    if (lane == 0) __hip_atomic_store(&prod[w + 1], (unsigned)(mpad + 1), RLX, WGS);
+    if (p.dbg != nullptr && lane == 0) {
         p.dbg[4 * s] = stamp0;
         p.dbg[4 * s + 1] = stamp1;
         p.dbg[4 * s + 2] = __builtin_amdgcn_s_memrealtime();
+        p.dbg[4 * s + 3] = __builtin_amdgcn_s_memtime() - clk0;  // shader clocks from chunk 1 to the end
     }
-    // the lane owning column n writes the final H' (cost = H' + phi(m, n))
-    if (ok && colok && jcol == p.n) p.out_last[0] = st.Hout;
 }
 
 // ----------------------------------------------------------------------------------
@@ -546,7 +607,7 @@ __device__ __forceinline__ unsigned cell_shifts(int sets, bool am) {
 }
 
 __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, int i, int j) {
-    const int s = (j - 1) >> 6, l = (j - 1) & 63, t = i - 1 + l;
+    const int s = (j - 1) >> 6, l = (j - 1) & 63, t = i - 1;
     const int spc = 16 / CB;
     const uint8_t* p = tb + (((long long)s * TC + t / spc) * 64 + l) * 16 + (t % spc) * CB;
     unsigned v = p[0];
@@ -563,52 +624,45 @@ constexpr int NSLOT = TB4 * TB4;
 __device__ __forceinline__ int slot_of(int ti, int tj) { return (ti & (TB4 - 1)) * TB4 + (tj & (TB4 - 1)); }
 __device__ __forceinline__ int torus_of(int i, int j) { return ((i - 1) & (TP - 1)) * TP + ((j - 1) & (TP - 1)); }
 
-// One loader wave decodes tile (ti, tj) into the torus: lane = column; each lane
-// walks the 16-byte chunks of its column's traceback stream that cover the
-// tile's 64 rows (the general path; one-byte words use load_tile_b1).
+// One loader wave decodes tile (ti, tj) into the torus: lane = column; the
+// tile's 64 rows of a column are 64/SPC whole 16-byte words of its stripe's
+// traceback stream (the general path; one-byte words use load_tile_b1).
 template <int CB>
 __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
                           int lane) {
     uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT;
     constexpr int SPC = 16 / CB;
-    constexpr int KMAX = TT / SPC + 1;
+    constexpr int KW = TT / SPC;
     const int i0 = ti * TT + 1;                       // first row of the tile
     const int j = tj * TT + lane + 1;                 // this lane's column
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const int bj = colok ? w.b[j - 1] : 0xfe;
-    const int tfirst = i0 - 1 + lane;                 // t of row i0 in this column
-    const int q0 = tfirst / SPC;
-    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC) * 64 + lane;
-    uint4 ch[KMAX];
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC + ti * KW) * 64 + lane;
+    const int nq = min(KW, w.TC - ti * KW);
+    uint4 ch[KW];
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
-        const int q = q0 + k;
-        ch[k] = (colok && q < w.TC) ? base[(long long)q * 64] : make_uint4(0, 0, 0, 0);
-    }
+    for (int k = 0; k < KW; k++) ch[k] = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
+    for (int k = 0; k < KW; k++) {
         const unsigned wd[4] = {ch[k].x, ch[k].y, ch[k].z, ch[k].w};
 #pragma unroll
         for (int u = 0; u < SPC; u++) {
-            const int r = (q0 + k) * SPC + u - tfirst;   // tile row
-            if (r >= 0 && r < TT) {
-                unsigned code = wd[(u * CB) >> 2] >> ((u * CB * 8) & 31);
-                if (CB == 1) code &= 0xffu;
-                else if (CB == 2) code &= 0xffffu;
-                dst[r * TP + lane] = (uint16_t)cell_shifts(sets_from_code(code, CB, w.o), sa[r] == bj);
-            }
+            const int r = k * SPC + u;   // tile row
+            unsigned code = wd[(u * CB) >> 2] >> ((u * CB * 8) & 31);
+            if (CB == 1) code &= 0xffu;
+            else if (CB == 2) code &= 0xffffu;
+            dst[r * TP + lane] = (uint16_t)cell_shifts(sets_from_code(code, CB, w.o), sa[r] == bj);
         }
     }
 }
 
 // One-byte traceback words (the common case, gap open < 7): branch-free decode.
-// A lane's 64 cells sit at byte offset (tfirst mod 16) of the five 16-byte
-// chunks it loads; the lane realigns them (dword select + v_alignbyte), folds
-// a_i == b_j into bit 7 of each word (SWAR zero-byte test on the staged a
-// bytes; words use bits 0-6) and decodes through a 256-entry table.
+// A lane's 64 cells are its four 16-byte words; it folds a_i == b_j into bit 7
+// of each word (SWAR zero-byte test on the staged a bytes; words use bits 0-6)
+// and decodes through a 256-entry table.
 __device__ void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
                              int lane) {
     uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT + lane;
@@ -617,14 +671,12 @@ __device__ void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t* torus,
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const unsigned bj = colok ? w.b[j - 1] : 0xfeu;
-    const int tfirst = i0 - 1 + lane;
-    const int q0 = tfirst >> 4, off = tfirst & 15;
-    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC) * 64 + lane;
-    unsigned wv[20];
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC + ti * 4) * 64 + lane;
+    const int nq = w.TC - ti * 4;
+    unsigned wv[16];
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const int q = q0 + k;
-        const uint4 c = (colok && q < w.TC) ? base[(long long)q * 64] : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < 4; k++) {
+        const uint4 c = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
         wv[4 * k] = c.x; wv[4 * k + 1] = c.y; wv[4 * k + 2] = c.z; wv[4 * k + 3] = c.w;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
@@ -636,18 +688,12 @@ __device__ void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t* torus,
         const uint4 x = sa4[k];
         av[4 * k] = x.x; av[4 * k + 1] = x.y; av[4 * k + 2] = x.z; av[4 * k + 3] = x.w;
     }
-    const int dw = off >> 2;
-    const unsigned sb = (unsigned)(off & 3);
-    unsigned al[17];
-#pragma unroll
-    for (int k = 0; k < 17; k++) al[k] = dw == 0 ? wv[k] : dw == 1 ? wv[k + 1] : dw == 2 ? wv[k + 2] : wv[k + 3];
     const unsigned bj4 = bj * 0x01010101u;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        unsigned cw = __builtin_amdgcn_alignbyte(al[k + 1], al[k], sb);  // rows 4k .. 4k+3
         const unsigned x = av[k] ^ bj4;
         const unsigned t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;      // bit 7 of a byte clear <=> byte == 0
-        cw = (cw & 0x7f7f7f7fu) | (~t & 0x80808080u);
+        const unsigned cw = (wv[k] & 0x7f7f7f7fu) | (~t & 0x80808080u);
 #pragma unroll
         for (int u = 0; u < 4; u++) dst[(4 * k + u) * TP] = lut[(cw >> (8 * u)) & 0xffu];
     }
@@ -1006,51 +1052,40 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
         boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, big, GVp, GHp, top, left, bnd_row, bnd_col, meta);
 }
 
-size_t fill_lds_bytes(int CB, int qbytes, bool tb, int K) {
-    const int spc = 16 / CB;
-    return (size_t)(tb ? FillLds::QRING_TB : FillLds::QRING_NOTB) + (size_t)K * (QROWS + spc) * qbytes;
+size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows) {
+    return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * qrows * qbytes;
 }
 
-template <int CB, typename QT, bool TB, bool FULL, int ABL>
+template <int CB, typename QT, bool TB, bool FULL, int NWC>
 static void launch_one(hipStream_t s, const FillArgs& p) {
-    const size_t lds = fill_lds_bytes(CB, (int)sizeof(QT), TB, p.K);
-    auto* fn = fill_kernel<CB, QT, TB, FULL, ABL>;
+    const size_t lds = std::max<size_t>(fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), FILL_LDS_MIN);
+    auto* fn = fill_kernel<CB, QT, TB, FULL, NWC>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    fn<<<dim3(p.nslabs), dim3(64 * (NW + 2)), lds, s>>>(p);
+    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
 
-template <int CB, typename QT>
-static void launch_fill_t(hipStream_t s, const FillArgs& p, bool tb, bool full) {
-    if (full) launch_one<CB, QT, true, true, 0>(s, p);
-    else if (tb) launch_one<CB, QT, true, false, 0>(s, p);
-    else launch_one<CB, QT, false, false, 0>(s, p);
+template <typename QT, int NWC>
+static void launch_fill_t(hipStream_t s, const FillArgs& p, int CB, bool tb, bool full) {
+    if (!tb) return launch_one<1, QT, false, false, NWC>(s, p);
+    if (full) {
+        if (CB == 1) launch_one<1, QT, true, true, NWC>(s, p);
+        else if (CB == 2) launch_one<2, QT, true, true, NWC>(s, p);
+        else launch_one<4, QT, true, true, NWC>(s, p);
+        return;
+    }
+    if (CB == 1) launch_one<1, QT, true, false, NWC>(s, p);
+    else if (CB == 2) launch_one<2, QT, true, false, NWC>(s, p);
+    else launch_one<4, QT, true, false, NWC>(s, p);
 }
 
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full) {
-    if (qbytes == 1) {
-        if (CB == 1) launch_fill_t<1, int8_t>(s, p, tb, full);
-        else if (CB == 2) launch_fill_t<2, int8_t>(s, p, tb, full);
-        else launch_fill_t<4, int8_t>(s, p, tb, full);
+    if (p.nwc == 4) {
+        if (qbytes == 1) launch_fill_t<int8_t, 4>(s, p, CB, tb, full);
+        else launch_fill_t<int16_t, 4>(s, p, CB, tb, full);
     } else {
-        if (CB == 1) launch_fill_t<1, int16_t>(s, p, tb, full);
-        else if (CB == 2) launch_fill_t<2, int16_t>(s, p, tb, full);
-        else launch_fill_t<4, int16_t>(s, p, tb, full);
+        if (qbytes == 1) launch_fill_t<int8_t, 8>(s, p, CB, tb, full);
+        else launch_fill_t<int16_t, 8>(s, p, CB, tb, full);
     }
-}
-
-// diagnostic ablation launcher (CB=1, int8 profile only)
-void launch_fill_ablation(hipStream_t s, const FillArgs& p, bool tb, int abl) {
-#define GA_ABL_CASE(A)                                          \
-    case A:                                                     \
-        if (tb) launch_one<1, int8_t, true, false, A>(s, p);    \
-        else launch_one<1, int8_t, false, false, A>(s, p);      \
-        break;
-    switch (abl) {
-        GA_ABL_CASE(0) GA_ABL_CASE(1) GA_ABL_CASE(2) GA_ABL_CASE(4) GA_ABL_CASE(8) GA_ABL_CASE(16) GA_ABL_CASE(17)
-        GA_ABL_CASE(21) GA_ABL_CASE(29) GA_ABL_CASE(31)
-        default: break;
-    }
-#undef GA_ABL_CASE
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {

@@ -1,7 +1,7 @@
 """Diagnostic: per-stripe timestamps of one fill (s_memrealtime, 100 MHz).
 
     python tools/fill_stamps.py [m] [n] [--tb]
-Prints the stripe start lag (ramp), per-stripe duration and the implied step time."""
+Prints the stripe start lag (ramp), per-stripe duration and the implied time per row."""
 import ctypes as C
 import json
 import os
@@ -34,17 +34,23 @@ t0 = st[:, 0].min()
 start, mid, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0, (st[:, 2] - t0) / 100.0  # microseconds
 f_ms = eng.kernel_ms()[0]
 dur = end - start
-step_ns = dur * 1e3 / (m + 63)
+step_ns = dur * 1e3 / m
+nwc = 4 if ns <= 4 * 256 else 8  # compute waves per workgroup (ga_host.cpp load_problem)
 out = {
     "m": m, "n": n, "tb": tb, "cost": cost, "fill_kernel_ms": f_ms, "nstripes": ns,
     "last_stripe_start_us": float(start[-1]), "last_end_us": float(end.max()),
     "lag_per_stripe_us_mean": float(np.mean(np.diff(start))),
-    "lag_intra_slab_us": float(np.mean([start[k + 1] - start[k] for k in range(ns - 1) if (k + 1) % 7 != 0])),
-    "lag_cross_slab_us": float(np.mean([start[k + 1] - start[k] for k in range(ns - 1) if (k + 1) % 7 == 0])),
+    "lag_intra_slab_us": float(np.mean([start[k + 1] - start[k] for k in range(ns - 1) if (k + 1) % nwc != 0])),
+    "lag_cross_slab_us": float(np.mean([start[k + 1] - start[k] for k in range(ns - 1) if (k + 1) % nwc == 0])),
     "stripe_duration_us_median": float(np.median(dur)),
-    "step_ns_median": float(np.median(step_ns)),
+    "row_ns_median": float(np.median(step_ns)),
     "first_half_vs_second_half": float(np.median((mid - start) / np.maximum(end - mid, 1e-9))),
     "start_us_samples": [float(x) for x in start[:: max(1, ns // 12)]],
+    # shader clocks (s_memtime) over the same span as end - start: the in-kernel clock and cycles per row
+    "clock_ghz_median": float(np.median(st[:, 3] / np.maximum(dur * 1e3, 1e-9))),
+    "cycles_per_row_median": float(np.median(st[:, 3] / m)),
+    "first_stripes_row_ns": [float(x) for x in step_ns[:10]],
+    "row_ns_min": float(np.min(step_ns)),
 }
 # one align for the walk diagnostics
 import random  # noqa: E402
@@ -52,7 +58,7 @@ random.seed(0)
 if tb:
     eng.align(np.array(random.getstate()[1], dtype=np.uint32), s1, s2)
     L.ga_debug_walk.argtypes = [C.c_void_p, C.c_void_p]
-    w2 = np.zeros(2, dtype=np.int32)
+    w2 = np.zeros(8, dtype=np.int32)
     L.ga_debug_walk(eng._h, w2.ctypes.data)
     out["walk"] = dict(eng.timings(), tile_wait_sleeps=int(w2[0]), tiles=int(w2[1]))
 print(json.dumps(out))
