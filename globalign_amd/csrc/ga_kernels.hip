@@ -229,20 +229,25 @@ template <typename T>
 __device__ __forceinline__ unsigned lds_addr(T* p) {
     return (unsigned)(uintptr_t)(__attribute__((address_space(3))) T*)p;
 }
-// single-lane LDS stores with a narrowed exec mask (no branch: the compute loop keeps
-// scalar control flow; a structured `if (lane == k)` turns uniform values into VGPR phis)
+// A compute wave's publication of four rows, one lane with a narrowed exec mask (no branch:
+// the compute loop keeps scalar control flow; a structured `if (lane == k)` turns uniform
+// values into VGPR phis): the lane owning the stripe's right edge writes the ring rows,
+// then {cons, prod} in one 8-byte store.  LDS executes one wave's operations in order,
+// so the rows land before the counters.
 typedef int v4i __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void lds_store_lane0(unsigned addr, unsigned v) {
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lds_publish(unsigned ring_addr, unsigned pc_addr, unsigned long long lanemask, v4i a,
+                                            v4i b, unsigned cons, unsigned prod) {
     unsigned long long saved;
-    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\tds_write_b32 %1, %2\n\ts_mov_b64 exec, %0"
-                 : "=&s"(saved) : "v"(addr), "v"(v) : "memory");
+    const v2u cp = {cons, prod};
+    asm volatile(
+        "s_mov_b64 %0, exec\n\ts_mov_b64 exec, %3\n\t"
+        "ds_write_b128 %1, %4\n\tds_write_b128 %1, %5 offset:16\n\tds_write_b64 %2, %6\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(ring_addr), "v"(pc_addr), "s"(lanemask), "v"(a), "v"(b), "v"(cp)
+        : "memory");
 }
-__device__ __forceinline__ void lds_store2_b128_lane(unsigned addr, unsigned long long lanemask, v4i a, v4i b) {
-    unsigned long long saved;
-    asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %2\n\tds_write_b128 %1, %3\n\tds_write_b128 %1, %4 offset:16\n\ts_mov_b64 exec, %0"
-                 : "=&s"(saved) : "v"(addr), "s"(lanemask), "v"(a), "v"(b) : "memory");
-}
-
 
 // LDS: counters | ring[NWC+1][RING] (int2) | qring[K][qrows] (QT)
 //   ring k feeds compute wave k (ring 0 from the IO wave, ring k+1 from wave k; the IO
@@ -251,8 +256,10 @@ __device__ __forceinline__ void lds_store2_b128_lane(unsigned addr, unsigned lon
 //   V~ = h1' - o, one broadcast 8-byte read per row.
 //   prod[k] = P: slots of rows <= P are written (the H' of row P itself lands with row P+1);
 //   cons[k] = C: the reader of ring k no longer needs slots < C;
+//   both live in one array, prodcons[2k] = cons[k], prodcons[2k+1] = prod[k+1], so compute
+//   wave k publishes both with one 8-byte store (prod[0] is written by the IO wave);
 //   prodq = Q: query-profile rows <= Q are written (the IO wave runs it ahead of the edges).
-enum { CI_PROD = 0, CI_CONS = 16, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
+enum { CI_PC = 0, CI_PROD0 = 31, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
 constexpr int FILL_CNT_BYTES = 256;
 
 template <int CB, typename QT, bool TB, bool FULL, int NWC>
@@ -262,8 +269,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
     int2* ring = reinterpret_cast<int2*>(smem + FILL_CNT_BYTES);
     QT* qring = reinterpret_cast<QT*>(ring + (NWC + 1) * RING);
-    unsigned* prod = cnt + CI_PROD;
-    unsigned* cons = cnt + CI_CONS;
+    // prod[k] (k >= 1) and cons[k] interleaved (see above); prod[0] apart
+    struct PC {
+        unsigned* c;
+        __device__ unsigned& prod(int k) { return k == 0 ? c[CI_PROD0] : c[2 * k - 1]; }
+        __device__ unsigned& cons(int k) { return c[2 * k]; }
+    } pc{cnt};
     unsigned* abort_sh = cnt + CI_ABORT;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave index: uniform
@@ -296,10 +307,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             bool moved = false;
             if (q_next < (unsigned)m) {
                 // profile rows of chunks the slowest wave (ring nlive's producer) has finished are free
-                const unsigned pl = lds_ld(&prod[nlive]);
+                const unsigned pl = lds_ld(&pc.prod(nlive));
                 const unsigned space = (pl & ~(unsigned)(FROWS - 1)) + QR - FROWS;
                 const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
-                if (hi > q_next) {
+                // whole 64-row batches (or the tail): the IO wave shares a SIMD with compute wave 0
+                if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
                     const unsigned r = q_next + 1 + lane;
                     if (r <= hi) {
                         const int x = p.a[r - 1];
@@ -314,7 +326,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             }
             if (in_next < (unsigned)m) {
                 // ring 0 slots are free below cons[0]
-                const unsigned space = lds_ld(&cons[0]) + RING;
+                const unsigned space = lds_ld(&pc.cons(0)) + RING;
                 const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
@@ -325,14 +337,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                         rin0[(r - 1) & RMASK] = make_int2(h0, e1.y - o);
                     }
                     // rows past m are padding (garbage nobody reads back)
-                    if (lane == 0) lds_st(&prod[0], hi == (unsigned)m ? (unsigned)mpad : hi);
+                    if (lane == 0) lds_st(&pc.prod(0), hi == (unsigned)m ? (unsigned)mpad : hi);
                     in_next = hi;
                     moved = true;
                 }
             }
             if (out_next < (unsigned)m) {
                 // row r of the right edge: H' from slot r (row r+1's entry), V~ from slot r-1
-                const unsigned P = lds_ld(&prod[nlive]);
+                const unsigned P = lds_ld(&pc.prod(nlive));
                 const unsigned hi = min(min(P, (unsigned)mpad + 1u) - 1u, min((unsigned)m, out_next + 64));
                 if (P > 0 && hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
                     const unsigned r = out_next + 1 + lane;
@@ -346,7 +358,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                         g_st(p.hand_prog + g, hi);
                         if (p.edge_prog != nullptr && last_slab)
                             __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
-                        lds_st(&cons[nlive], hi - 1u);
+                        lds_st(&pc.cons(nlive), hi - 1u);
                     }
                     out_next = hi;
                     moved = true;
@@ -370,6 +382,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     if (w >= nlive) return;
 
     // ---------------- compute wave w: stripe s ----------------
+    // compute waves win VALU arbitration against the IO wave on their SIMD (the chain head,
+    // wave 0, shares one with it)
+    __builtin_amdgcn_s_setprio(2);
     const int s = g * NWC + w;
     const int j0 = s * 64;                    // columns j0+1 .. j0+64
     const int jcol = j0 + lane + 1;
@@ -389,8 +404,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     uint4* tbw = TB ? reinterpret_cast<uint4*>(p.tb) + (long long)s * p.TC * 64 + lane : nullptr;
     unsigned avail = 0, outfree = 0, qavail = 0;
     unsigned long long stamp0 = 0, stamp1 = 0, clk0 = 0;
-    const unsigned prod_out_lds = lds_addr(&prod[w + 1]);
-    const unsigned cons_lds = lds_addr(&cons[w]);
+    const unsigned pc_lds = lds_addr(&pc.cons(w));  // {cons[w], prod[w + 1]}
     const unsigned rout_lds = lds_addr(rout);
     const unsigned long long srcmask = 1ull << srcl;
     // wait (wave-uniform) until *ctr + add >= target.  A wait that gives up (the workgroup
@@ -408,12 +422,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         // the reads of what the counter guards stay after it (the LDS itself keeps order)
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
-    wait_ge(&prod[w], 0, avail, 4);  // rows 1..4 before the first edge read
+    wait_ge(&pc.prod(w), 0, avail, 4);  // rows 1..4 before the first edge read
     int4 e01 = reinterpret_cast<const int4*>(rin)[0];  // slots 0..3: (H'(i-1), V~(i)) of rows 1..4
     int4 e23 = reinterpret_cast<const int4*>(rin)[1];
     // the counter is read one sub-chunk before it is needed (a plain load: the asm stores'
     // memory clobbers keep the compiler from reusing an old value, and it waits at the use)
-    const unsigned* prod_in = &prod[w];
+    const unsigned* prod_in = &pc.prod(w);
     unsigned pnext = *prod_in;
 
     // traceback codes are software-pipelined one sub-chunk behind the DP chain, so their
@@ -427,10 +441,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         return min((unsigned)(pX[u] - pH[u]), op1) | (min((unsigned)(pY[u] - pH[u]), op1) << W) |
                (min((unsigned)(pM[u] - pH[u]), 1u) << (2 * W));
     };
-    auto store_words = [&](int cc, const uint32_t* wds) {
+    // the words of chunk cc at tbw; each chunk's CB 16-byte words per lane are 64 lanes apart
+    auto store_words = [&](const uint32_t* wds) {
 #pragma unroll
         for (int k = 0; k < CB; k++)
-            tbw[(long long)(cc * CB + k) * 64] = make_uint4(wds[4 * k], wds[4 * k + 1], wds[4 * k + 2], wds[4 * k + 3]);
+            tbw[k * 64] = make_uint4(wds[4 * k], wds[4 * k + 1], wds[4 * k + 2], wds[4 * k + 3]);
+        tbw += CB * 64;
     };
 
     for (int c = 0; c < nch; c++) {
@@ -441,7 +457,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         }
         if (p.dbg != nullptr && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
         // output ring slots row0 .. row0+FROWS (the tail write included) must be free
-        wait_ge(&cons[w + 1], RING, outfree, row0 + FROWS + 1);
+        wait_ge(&pc.cons(w + 1), RING, outfree, row0 + FROWS + 1);
         wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + FROWS);
         QPack<QT> q;
         q.load(qcol + ((unsigned)row0 & qmask));
@@ -496,7 +512,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                     // next sub-chunk's rows and read their edges, three rows before their use
                     if (r0 + 4 < mpad) {
                         avail = sgpr_u(max(avail, pnext));
-                        wait_ge(&prod[w], 0, avail, r0 + 8);
+                        wait_ge(&pc.prod(w), 0, avail, r0 + 8);
                     }
                     const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 4) & RMASK));
                     n01 = e4[0];
@@ -513,14 +529,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             for (int u = 0; u < 4; u++) { pM[u] = sM[u]; pX[u] = sX[u]; pY[u] = sY[u]; pH[u] = sH[u]; }
             if (TB && sc == 0) {
                 // the previous chunk's words are complete
-                if (c > 0) store_words(c - 1, accP);
+                if (c > 0) store_words(accP);
             }
             // the right edge of these rows goes out; LDS executes one wave's operations in
             // order: the rows land before the counters
-            lds_store2_b128_lane(rout_lds + (unsigned)(r0 & RMASK) * 8u, srcmask, v4i{oH[0], oV[0], oH[1], oV[1]},
-                                 v4i{oH[2], oV[2], oH[3], oV[3]});
-            lds_store_lane0(prod_out_lds, (unsigned)(r0 + 4));
-            lds_store_lane0(cons_lds, (unsigned)(r0 + 3));
+            lds_publish(rout_lds + (unsigned)(r0 & RMASK) * 8u, pc_lds, srcmask, v4i{oH[0], oV[0], oH[1], oV[1]},
+                        v4i{oH[2], oV[2], oH[3], oV[3]}, (unsigned)(r0 + 3), (unsigned)(r0 + 4));
             e01 = n01;
             e23 = n23;
         }
@@ -534,11 +548,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             const int pu = (12 + u) * CB;
             accP[pu >> 2] |= code_of(u) << (pu * 8 & 31);
         }
-        store_words(nch - 1, accP);
+        store_words(accP);
     }
     // H' of the last (padded) row, for the reader's hand-off of row m when m == mpad
     if (lane == srcl) rout[mpad & RMASK].x = Hprev;
-    if (lane == 0) __hip_atomic_store(&prod[w + 1], (unsigned)(mpad + 1), RLX, WGS);
+    if (lane == 0) __hip_atomic_store(&pc.prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
     if (p.dbg != nullptr && lane == 0) {
         p.dbg[4 * s] = stamp0;
         p.dbg[4 * s + 1] = stamp1;
