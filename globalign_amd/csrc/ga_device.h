@@ -55,6 +55,7 @@ struct WalkArgs {
     int maxh;             // the reference's move bound m + n (global n)
     uint32_t* ops;        // out: 2-bit levels, dispatch D at bits 30 - 2*(D & 15) of word D >> 4
     int* result;          // out: [D, i, j, reason, diagnostics...]
+    unsigned* dbg;        // optional: per tile need (ti, tj, D, wait ticks) x WALK_DBG entries, or nullptr
 };
 
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,

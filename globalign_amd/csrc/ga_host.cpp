@@ -281,7 +281,7 @@ struct ga_ctx {
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
     bool dbg_on = false;
     int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
-    DevBuf dbg;
+    DevBuf dbg, wdbg;
 };
 
 namespace {
@@ -530,6 +530,11 @@ int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st) 
     w.maxh = (int)(c->m + c->n_global);
     w.ops = c->ops.as<uint32_t>();
     w.result = c->result.as<int>();
+    if (c->dbg_on) {
+        HIPCHK(c->wdbg.ensure(sizeof(unsigned) * 4 * 8192));
+        HIPCHK(hipMemsetAsync(c->wdbg.p, 0xff, sizeof(unsigned) * 4 * 8192, c->stream));
+    }
+    w.dbg = c->dbg_on ? c->wdbg.as<unsigned>() : nullptr;
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     ga::launch_walk(c->stream, w);
     HIPCHK(hipGetLastError());
@@ -671,7 +676,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
-                      &c->result, &c->halo_in})
+                      &c->result, &c->halo_in, &c->dbg, &c->wdbg})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& e : c->ev)
@@ -839,6 +844,14 @@ int ga_last_kernel_ms(ga_ctx* c, float* fill_ms, float* walk_ms) {
     if (!c) return fail(GA_E_ARG, "null context");
     if (fill_ms) *fill_ms = c->fill_ms;
     if (walk_ms) *walk_ms = c->walk_ms;
+    return GA_OK;
+}
+
+// Diagnostics (not in the public header): the walk's tile-need records (ti, tj, D, wait ticks) x 8192.
+int ga_debug_walk_tiles(ga_ctx* c, unsigned* out) {
+    if (!c || !out) return fail(GA_E_ARG, "null argument");
+    if (!c->wdbg.p) return fail(GA_E_STATE, "no diagnostic walk ran");
+    HIPCHK(hipMemcpy(out, c->wdbg.p, sizeof(unsigned) * 4 * 8192, hipMemcpyDeviceToHost));
     return GA_OK;
 }
 
