@@ -134,11 +134,13 @@ def _recv_obj(dist, src, group):
     return box[0]
 
 
-def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_words, band=4096, torch=None):
+def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_words, band=4096, torch=None,
+                traceback=True):
     """Distributed fill + traceback of one problem.  Collective over all ranks.
 
     Returns (cost, (seq_1_aligned, middle, seq_2_aligned), status, mt_words_after) on rank 0, None elsewhere.
-    status: 0 ok, 1 the reference's IndexError."""
+    status: 0 ok, 1 the reference's IndexError.  With traceback=False only the fill runs and rank 0
+    returns (cost, None, 0, None) (dp_array_forward + min of the last cell, globaligner.py:366-425)."""
     rank, world = links.rank, links.world
     m, n = len(a_codes), len(b_codes)
     edges = slab_bounds(n, world)
@@ -154,11 +156,19 @@ def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_
         halo_out = torch.zeros(shape, dtype=dtype, pin_memory=pin)
     engine.slab_bind_halos(halo_in.data_ptr() if rank > 0 else 0, halo_out.data_ptr() if rank < world - 1 else 0,
                            halo_in, halo_out)
-    engine.slab_launch(traceback=True)
-    engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
+    engine.slab_launch(traceback=traceback)
+    if traceback:
+        engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
     stream_edges(dist, links, engine, halo_in, halo_out, m, band)
     cost = engine.slab_finish()
     ctrl = links.ctrl
+    if not traceback:
+        if world > 1:
+            if rank == world - 1:
+                _send_obj(dist, cost, 0, ctrl)
+            elif rank == 0:
+                cost = _recv_obj(dist, world - 1, ctrl)
+        return (cost, None, 0, None) if rank == 0 else None
     # ---- walk, right to left
     if rank == world - 1:
         state = [m, n, 0, 0, 0, 1, -1]
@@ -265,30 +275,29 @@ def init_process_group():
     return dist, rank, world, local
 
 
-def bench_main(args, wl, workloads, scoring):
-    """bench.py --gpus N (N > 1): weak scaling of the headline workload.
+def bench_main(args, wl, workload):
+    """bench.py --gpus N (N > 1): strong scaling of a workload over N GPUs.
 
-    Every GPU keeps the per-GPU work of the 1-GPU workload (m*n cells): the
-    matrix grows as a square, side = sqrt(N) * side_1, cut into N column
-    slabs; a step is the whole distributed fill + traceback of one pair."""
+    The SAME pair as the 1-GPU run (BASELINE C4 is the 1/2/4/8-GPU curve) is cut into N column
+    slabs; a step is the distributed fill (+ traceback for traceback workloads) of that pair."""
     import torch
     import bench
-    from globalign_amd import _native
     dist, rank, world, local = init_process_group()
     links = Links(dist, rank, world)
-    side = int(round(math.sqrt(world * wl["m"] * wl["n"])))
-    m = n = side
-    s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
-    tables, _ = bench.problem_tables(s1, s2)
+    m, n = wl["m"], wl["n"]
+    s1, s2 = bench.workload_pair(wl)
+    tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
     a_codes, b_codes = tables.codes(s1), tables.codes(s2)
     import random
     random.seed(0)
     mt0 = np.array(random.getstate()[1], dtype=np.uint32)
     engine = GpuSlabEngine(local % max(1, torch.cuda.device_count()))  # ranks may share a GPU (gloo rehearsal)
     result = None
+    band = 4096 if m <= 200_000 else 8192
 
     def step():
-        return align_slabs(dist, links, engine, s1, s2, a_codes, b_codes, tables, mt0, torch=torch)
+        return align_slabs(dist, links, engine, s1, s2, a_codes, b_codes, tables, mt0, band=band, torch=torch,
+                           traceback=wl["traceback"])
 
     for _ in range(args.warmup):
         result = step()
@@ -304,8 +313,11 @@ def bench_main(args, wl, workloads, scoring):
     dist.all_reduce(el, op=dist.ReduceOp.MAX, group=links.ctrl)
     elapsed = float(el.item())
     if rank == 0:
-        cost, (sa, _, sb), status, _ = result
-        assert status == 0 and sa.replace("-", "") == s1 and sb.replace("-", "") == s2
+        cost = result[0]
+        if wl["traceback"]:
+            _, (sa, _, sb), status, _ = result
+            assert status == 0 and sa.replace("-", "") == s1 and sb.replace("-", "") == s2
+        gold = bench.golden_cost(workload)
         cells = m * n
         line = {
             "metric": bench.METRIC,
@@ -316,13 +328,15 @@ def bench_main(args, wl, workloads, scoring):
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (SplitMix64 DNA, SURVEY 8d)",
-            "config": {"workload": f"{wl['desc']}; weak-scaled to {m} x {n} over {world} GPUs "
-                                   f"(column slabs, banded RCCL edge exchange, right-to-left walk hand-off)",
-                       "m": m, "n": n, "traceback": True, "parallelism": f"column slabs x{world}", "cost": cost},
+            "data": "synthetic (SplitMix64, SURVEY 8d)",
+            "config": {"workload": f"{wl['desc']}; {world} column slabs, banded RCCL edge exchange ({band}-row bands)"
+                                   + ("; right-to-left walk hand-off" if wl["traceback"] else ""),
+                       "m": m, "n": n, "traceback": wl["traceback"], "parallelism": f"column slabs x{world}",
+                       "cost": int(cost), "oracle_cost": gold,
+                       "cost_matches_oracle": (int(cost) == gold) if gold is not None else None},
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

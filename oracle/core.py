@@ -39,6 +39,8 @@ def lib():
         L.gao_fill_sets.argtypes = [u8p, I64, u8p, I64, i64p, C.c_int, i64p, i64p, I64, i64p, i64p, u16p, i64p]
         L.gao_fill_score.argtypes = [u8p, I64, u8p, I64, i64p, C.c_int, i64p, i64p, I64, i64p, i64p, i64p]
         L.gao_fill_slab.argtypes = [u8p, I64, u8p, I64, i64p, C.c_int, i64p, i64p, I64, i64p, i64p, i64p]
+        L.gao_fill_score_parallel.argtypes = [u8p, I64, u8p, I64, i64p, C.c_int, i64p, i64p, I64, i64p, i64p, C.c_int,
+                                              i64p]
         L.gao_traceback_full.argtypes = [i64p, I64, I64, I64, u8p, u8p, C.c_char_p, C.c_char_p, i64p, C.c_int,
                                          i64p, u32p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(I64), C.POINTER(I64)]
         L.gao_traceback_sets.argtypes = [u16p, i64p, i64p, I64, I64, I64, u8p, u8p, C.c_char_p, C.c_char_p, i64p,
@@ -93,6 +95,13 @@ def fill_full(tab, a, b, o, dp):
 def fill_score(tab, a, b, o, row0, col0):
     last = np.zeros(3, np.int64)
     lib().gao_fill_score(a, len(a), b, len(b), tab.sub, tab.K, tab.gh, tab.gv, o, row0, col0, last)
+    return last
+
+
+def fill_score_parallel(tab, a, b, o, row0, col0, threads=8):
+    """fill_score on `threads` host threads (column slabs x row bands wavefront); same cells (gao_cell)."""
+    last = np.zeros(3, np.int64)
+    lib().gao_fill_score_parallel(a, len(a), b, len(b), tab.sub, tab.K, tab.gh, tab.gv, o, row0, col0, threads, last)
     return last
 
 

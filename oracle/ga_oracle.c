@@ -18,7 +18,7 @@
  * dispatcher calls 18 times per traceback step.
  *
  * Parity pinning: tests/test_oracle.py checks every function here against the
- * golden fixtures tests/golden/*.json produced by running the reference itself
+ * golden fixtures the tests/golden JSON files produced by running the reference itself
  * (tests/golden/make_golden.py).
  */
 #include <stdint.h>
@@ -377,4 +377,75 @@ void gao_mt_draws(uint32_t* mt_state, int nsizes, const int* sizes, int* out) {
     for (int k = 0; k < nsizes; k++) out[k] = randbelow(&rng, sizes[k]);
     memcpy(mt_state, rng.mt, sizeof(uint32_t) * MT_N);
     mt_state[MT_N] = (uint32_t)rng.mti;
+}
+
+/* Score-only fill on T host threads (test infrastructure: pins the C4 cost).
+ * Column slabs, one per thread; row bands of B rows.  Thread k fills band r of its
+ * slab once thread k-1 has published band r of its right column (a wavefront
+ * over slabs).  Every cell is gao_cell, the literal get_next_best_costs. */
+#include <pthread.h>
+#include <stdatomic.h>
+
+typedef struct {
+    const uint8_t* a; i64 m; const uint8_t* b; i64 n; const i64* sub; int K; const i64* gh; const i64* gv; i64 o;
+    const i64* row0; const i64* col0;
+    int T; i64 B; i64* edges;         /* [T+1][m+1][3]: edge k = left column of slab k */
+    _Atomic i64* done;                /* [T]: rows of slab k's right edge published */
+    i64* last;
+} par_t;
+
+typedef struct { par_t* p; int k; } par_arg;
+
+static void* par_worker(void* vp) {
+    par_arg* pa = (par_arg*)vp;
+    par_t* p = pa->p;
+    const int k = pa->k;
+    const i64 c0 = p->n * k / p->T, c1 = p->n * (k + 1) / p->T, w = c1 - c0;
+    i64* prev = (i64*)malloc(sizeof(i64) * 3 * (w + 1));
+    i64* cur = (i64*)malloc(sizeof(i64) * 3 * (w + 1));
+    memcpy(prev, &p->row0[3 * c0], sizeof(i64) * 3 * (w + 1));
+    const i64* left = p->edges + (size_t)k * 3 * (p->m + 1);
+    i64* right = p->edges + (size_t)(k + 1) * 3 * (p->m + 1);
+    memcpy(&right[0], &p->row0[3 * c1], sizeof(i64) * 3);
+    for (i64 r0 = 1; r0 <= p->m; r0 += p->B) {
+        const i64 r1 = r0 + p->B - 1 < p->m ? r0 + p->B - 1 : p->m;
+        if (k > 0)
+            while (atomic_load_explicit(&p->done[k - 1], memory_order_acquire) < r1) sched_yield();
+        for (i64 i = r0; i <= r1; i++) {
+            memcpy(cur, &left[3 * i], sizeof(i64) * 3);
+            const uint8_t ai = p->a[i - 1];
+            for (i64 j = 1; j <= w; j++)
+                gao_cell(&prev[3 * (j - 1)], &cur[3 * (j - 1)], &prev[3 * j], p->sub[ai * p->K + p->b[c0 + j - 1]],
+                         p->gh[p->b[c0 + j - 1]], p->gv[ai], p->o, &cur[3 * j]);
+            memcpy(&right[3 * i], &cur[3 * w], sizeof(i64) * 3);
+            i64* t = prev; prev = cur; cur = t;
+        }
+        atomic_store_explicit(&p->done[k], r1, memory_order_release);
+    }
+    if (k == p->T - 1) memcpy(p->last, &prev[3 * w], sizeof(i64) * 3);
+    free(prev);
+    free(cur);
+    return NULL;
+}
+
+void gao_fill_score_parallel(const uint8_t* a, i64 m, const uint8_t* b, i64 n, const i64* sub, int K, const i64* gh,
+                             const i64* gv, i64 o, const i64* row0, const i64* col0, int T, i64* last) {
+    if (T < 1) T = 1;
+    if (T > n) T = (int)n;
+    par_t p = {a, m, b, n, sub, K, gh, gv, o, row0, col0, T, 256, NULL, NULL, last};
+    p.edges = (i64*)malloc(sizeof(i64) * 3 * (size_t)(m + 1) * (T + 1));
+    memcpy(p.edges, col0, sizeof(i64) * 3 * (m + 1));
+    p.done = (_Atomic i64*)calloc(T, sizeof(i64));
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * T);
+    par_arg* args = (par_arg*)malloc(sizeof(par_arg) * T);
+    for (int k = 0; k < T; k++) {
+        args[k].p = &p;
+        args[k].k = k;
+        pthread_create(&th[k], NULL, par_worker, &args[k]);
+    }
+    for (int k = 0; k < T; k++) pthread_join(th[k], NULL);
+    free(th);
+    free(args);
+    free((void*)p.done);
+    free(p.edges);
 }

@@ -172,7 +172,7 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path):
+def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True):
     import torch
     import torch.distributed as dist
     from globalign_amd import distributed
@@ -186,24 +186,28 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path):
         links = distributed.Links(dist, rank, world)
         eng = OracleSlabEngine(cmat, goc)
         res = distributed.align_slabs(dist, links, eng, seq_1, seq_2, tables.codes(seq_1), tables.codes(seq_2),
-                                      tables, mt_words, band=band, torch=torch)
+                                      tables, mt_words, band=band, torch=torch, traceback=traceback)
         if rank == 0:
             cost, strings, status, mt_after = res
-            np.savez(out_path, cost=cost, a=strings[0], mid=strings[1], b=strings[2], status=status,
-                     mt=np.asarray(mt_after, dtype=np.uint32))
+            if traceback:
+                np.savez(out_path, cost=cost, a=strings[0], mid=strings[1], b=strings[2], status=status,
+                         mt=np.asarray(mt_after, dtype=np.uint32))
+            else:
+                assert strings is None and mt_after is None
+                np.savez(out_path, cost=cost, status=status)
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, m, n, seed, band, tmp_path):
+def _run(world, m, n, seed, band, tmp_path, traceback=True):
     import torch.multiprocessing as mp
     seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
     random.seed(seed)
     mt_words = np.array(random.getstate()[1], dtype=np.uint32)
     out = str(tmp_path / f"res_{world}_{seed}.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out), nprocs=world,
-                       join=True, start_method="fork")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out, traceback),
+                       nprocs=world, join=True, start_method="fork")
     return seq_1, seq_2, mt_words, np.load(out)
 
 
@@ -217,6 +221,16 @@ def test_slabs_match_single_problem_oracle(world, m, n, seed, band, tmp_path):
     assert (str(r["a"]), str(r["mid"]), str(r["b"])) == tuple(ref["strings"])
     assert int(r["status"]) == 0
     assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+
+
+@pytest.mark.parametrize("world,m,n,seed,band", [(2, 180, 300, 7, 50), (4, 120, 420, 9, 32)])
+def test_slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
+    """The strong-scaling bench path (C4): fill + score only, no walk; the cost equals the single-problem oracle."""
+    from oracle import core
+    seq_1, seq_2, mt_words, r = _run(world, m, n, seed, band, tmp_path, traceback=False)
+    cmat, goc = _scoring(seq_1, seq_2)
+    ref = core.align(seq_1, seq_2, cmat, goc, mt_words)
+    assert int(r["cost"]) == ref["cost"] and int(r["status"]) == 0
 
 
 def test_slab_bounds_and_bands():

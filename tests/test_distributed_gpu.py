@@ -33,7 +33,7 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path):
+def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True):
     import torch
     import torch.distributed as dist
     from globalign_amd import distributed
@@ -48,11 +48,15 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path):
         eng = distributed.GpuSlabEngine(0)
         for _ in range(2):  # the second run reuses the context (buffers, progress words)
             res = distributed.align_slabs(dist, links, eng, seq_1, seq_2, tables.codes(seq_1),
-                                          tables.codes(seq_2), tables, mt_words, band=band, torch=torch)
+                                          tables.codes(seq_2), tables, mt_words, band=band, torch=torch,
+                                          traceback=traceback)
         if rank == 0:
             cost, strings, status, mt_after = res
-            np.savez(out_path, cost=cost, a=strings[0], mid=strings[1], b=strings[2], status=status,
-                     mt=np.asarray(mt_after, dtype=np.uint32))
+            if traceback:
+                np.savez(out_path, cost=cost, a=strings[0], mid=strings[1], b=strings[2], status=status,
+                         mt=np.asarray(mt_after, dtype=np.uint32))
+            else:
+                np.savez(out_path, cost=cost, status=status)
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -74,3 +78,26 @@ def test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path):
     assert int(r["cost"]) == ref["cost"]
     assert (str(r["a"]), str(r["mid"]), str(r["b"])) == tuple(ref["strings"])
     assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+
+
+@pytest.mark.parametrize("world,m,n,seed,band", [(2, 4000, 60_000, 41, 1024), (3, 3000, 40_000, 43, 600)])
+def test_gpu_slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
+    """Strong-scaling bench path (C4 shape): score only, each rank's slab many workgroup slabs (60k columns
+    over 2 ranks = 2 x 118 workgroups).  The ranks share one GPU here, so all their workgroups must be
+    co-resident (<= 256 CUs; each rank's first slab waits on the other rank).  Cost vs the C oracle."""
+    import torch.multiprocessing as mp
+    from oracle import core
+    from globalign_amd._native import CostTables
+    seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
+    random.seed(seed)
+    mt_words = np.array(random.getstate()[1], dtype=np.uint32)
+    out = str(tmp_path / "res_so.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out, False), nprocs=world,
+                       join=True, start_method="spawn")
+    r = np.load(out)
+    cmat, goc = _scoring(seq_1, seq_2)
+    tab = core.Tables(cmat)
+    a, b = tab.codes(seq_1), tab.codes(seq_2)
+    big = (tab.max_cost + 1) * max(m, n)
+    row0, col0 = core.boundary(tab, a, b, goc, big)
+    assert int(r["cost"]) == int(min(core.fill_score_parallel(tab, a, b, goc, row0, col0, 4)))

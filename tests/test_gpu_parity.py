@@ -223,3 +223,50 @@ def _fast_splitmix(length, seed, alphabet="dna"):
 def test_fast_splitmix_matches_reference_generator():
     assert _fast_splitmix(500, 1) == splitmix_seq(500, 1, "dna")
     assert _fast_splitmix(300, 4, "protein") == splitmix_seq(300, 4, "protein")
+
+
+def _rescore(r):
+    """Cost of an emitted alignment recomputed from its strings (affine gaps: open paid per gap run)."""
+    C, o = r.costing_mat, r.gap_open_cost
+    cost, prev = 0, None
+    for x, y in zip(r.seq_1_aligned, r.seq_2_aligned):
+        kind = 0 if (x != "-" and y != "-") else (1 if x == "-" else 2)
+        cost += C[x][y] if kind == 0 else (C["-"][y] if kind == 1 else C[x]["-"])
+        if kind != 0 and kind != prev:
+            cost += o
+        prev = kind
+    return cost
+
+
+def test_multi_round_slabs_vs_oracle(ga):
+    """More workgroup slabs than CUs (ticket-ordered rounds, as C4 runs on one GPU): 1000 x 200k DNA is
+    3125 stripes = 391 slabs of 8 waves.  Cost vs the C oracle's O(n)-memory fill; the alignment must
+    re-derive both sequences and rescore to the same cost."""
+    from oracle import core
+    s1, s2 = _fast_splitmix(1000, 31), _fast_splitmix(200_000, 32)
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+    random.seed(4)
+    r = ga.GlobalAligner(max_seq_len_prod=None, **kw).align(s1, s2)
+    tab = core.Tables(r.costing_mat)
+    a, b = tab.codes(s1), tab.codes(s2)
+    big = (tab.max_cost + 1) * 200_000
+    row0, col0 = core.boundary(tab, a, b, r.gap_open_cost, big)
+    assert r.cost == int(min(core.fill_score(tab, a, b, r.gap_open_cost, row0, col0)))
+    assert r.seq_1_aligned.replace("-", "") == s1 and r.seq_2_aligned.replace("-", "") == s2
+    assert _rescore(r) == r.cost
+
+
+def test_tall_narrow_vs_oracle(ga):
+    """200k x 1000 (16 stripes, 4 slabs): long stripes, many 16-row chunks, ring wrap-around."""
+    from oracle import core
+    s1, s2 = _fast_splitmix(200_000, 33), _fast_splitmix(1000, 34)
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+    random.seed(5)
+    r = ga.GlobalAligner(max_seq_len_prod=None, **kw).align(s1, s2)
+    tab = core.Tables(r.costing_mat)
+    a, b = tab.codes(s1), tab.codes(s2)
+    big = (tab.max_cost + 1) * 200_000
+    row0, col0 = core.boundary(tab, a, b, r.gap_open_cost, big)
+    assert r.cost == int(min(core.fill_score(tab, a, b, r.gap_open_cost, row0, col0)))
+    assert r.seq_1_aligned.replace("-", "") == s1 and r.seq_2_aligned.replace("-", "") == s2
+    assert _rescore(r) == r.cost
