@@ -270,3 +270,43 @@ def test_tall_narrow_vs_oracle(ga):
     assert r.cost == int(min(core.fill_score(tab, a, b, r.gap_open_cost, row0, col0)))
     assert r.seq_1_aligned.replace("-", "") == s1 and r.seq_2_aligned.replace("-", "") == s2
     assert _rescore(r) == r.cost
+
+
+# ---------------------------------------------------------------- bench workloads vs the oracle's cost goldens
+@pytest.mark.parametrize("name", ["c2", "c5", "c3", "c4"])
+def test_bench_workload_cost_matches_golden(ga, name):
+    """Each bench.py workload at its full BASELINE size (C4 = 10^12 cells, score only) against the cost
+    the threaded C oracle produced (tests/golden/make_cost_golden.py, make_c4_golden.py); traceback
+    workloads also walk and must reproduce both inputs."""
+    import bench
+    from globalign_amd import _native
+    wl = bench.WORKLOADS[name]
+    gold = json.load(open(os.path.join(GOLDEN, f"{name}_cost.json")))["cost"]
+    s1, s2 = bench.workload_pair(wl)
+    tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(s1), tables.codes(s2), tables)
+        if wl["traceback"]:
+            random.seed(0)
+            mt = np.array(random.getstate()[1], dtype=np.uint32)
+            cost, (a, _, b), status, _ = eng.align(mt, s1, s2)
+            assert status == 0 and a.replace("-", "") == s1 and b.replace("-", "") == s2
+        else:
+            cost = eng.fill(traceback=False)[0]
+    finally:
+        eng.close()
+    assert int(cost) == gold
+
+
+@pytest.mark.parametrize("div,lens", [(0.0, (3000, 3400)), (0.05, (4000, 4000)), (0.3, (2500, 2000))])
+def test_similar_pairs_vs_oracle(ga, monkeypatch, div, lens):
+    """Similar pairs from draw_two_random_seqs (reference start.py:724-867): long diagonal runs with
+    sparse indels, the opposite of the i.i.d. inputs -- long match streaks through the walk."""
+    from globalign_amd.random_seqs import draw_two_random_seqs
+    orig = random.seed
+    monkeypatch.setattr(random, "seed", lambda a=None, version=2: orig(4242 if a is None else a, version))
+    s1, s2 = draw_two_random_seqs(list("ACGT"), lens[0], lens[0], lens[1], lens[1], div, 41, 42)
+    monkeypatch.setattr(random, "seed", orig)
+    _oracle_case(ga, s1, s2, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1),
+                 seed=int(div * 100) + 1)

@@ -152,3 +152,14 @@ def test_pyport_matches_oracle():
         a, mid, b, cost = pyport.traceback(T, s1, s2, cmat, goc)
         assert cost == ref["cost"] and (a, mid, b) == ref["strings"]
         assert state_digest() == state_digest(core.mt_state_tuple(ref["mt_out"]))
+
+
+def test_oracle_reproduces_c2_cost_golden():
+    """The threaded score-only fill that pins the bench workloads' costs (tests/golden/*_cost.json),
+    re-run at C2 (10^8 cells, well under a second)."""
+    import json
+    import os
+    from tests.golden.make_cost_golden import cost_of
+    import bench
+    gold = json.load(open(os.path.join(GOLDEN, "c2_cost.json")))["cost"]
+    assert cost_of(bench.WORKLOADS["c2"], 4) == gold
