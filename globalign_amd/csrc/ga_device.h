@@ -32,6 +32,7 @@ struct FillArgs {
     int* full;                // FULL output (shifted M', X', Y') or nullptr
     int m, n, o, nstripes, nslabs, TC;  // TC: 16-byte traceback words per lane per stripe
     int nwc, qrows;                     // compute waves per workgroup; LDS query-profile ring rows
+    int cols_per_lane;                  // T: columns per lane (a stripe is 64*T columns; 1, 2 or 4)
     unsigned spin_limit, halo_spin_limit;
     unsigned long long* dbg;  // optional timestamps: [nstripes][4] (s_memrealtime) or nullptr
 };

@@ -263,6 +263,7 @@ struct ga_ctx {
     int64_t n_global = 0, col0 = 0;
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
+    int T = 1, T_req = 0, nwc_req = 0;      // columns per lane of the fill (T_req 0: automatic; GA_COLS_PER_LANE)
     int64_t GV_m = 0, GH_n = 0;
     std::vector<uint8_t> h_a, h_b;
     // device buffers
@@ -291,6 +292,35 @@ int check_ctx(ga_ctx* c) {
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) return fail(GA_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
     return GA_OK;
+}
+
+// Stripe geometry: T columns per lane (a stripe = one compute wave = 64*T columns).
+// Blocked stripes pay the wave scan, the edge traffic and the control once per 64*T cells, but
+// leave fewer stripes (waves) to fill the chip and lengthen each row's dependent chain.  A
+// workgroup chains 4 waves (one per SIMD) when every stripe gets a wave that way, else 8.
+void set_stripes(ga_ctx* c, int T_req, bool tb, bool full) {
+    const int64_t simds = 4 * (int64_t)c->num_cu;
+    // the FULL debug output is T == 1 only; T == 8 is score only (register budget)
+    const int cap = full ? 1 : tb ? 4 : 8;
+    int T = 1;
+    if (T_req == 1 || T_req == 2 || T_req == 4 || T_req == 8) {
+        T = std::min(T_req, cap);
+    } else {
+        // the widest stripes that still leave >= 1.5 waves per SIMD (measured: 1M columns score
+        // only T = 8 > 4 > 2 > 1; 100k columns with traceback T = 1 > 2 > 4)
+        for (int t = cap; t > 1; t /= 2)
+            if ((c->n + 64 * t - 1) / (64 * t) * 2 >= 3 * simds) {
+                T = t;
+                break;
+            }
+    }
+    // a slab with a right neighbour hands column n on: its last stripe must be whole (T == 1
+    // takes the edge from any lane)
+    while (T > 1 && c->col0 + c->n < c->n_global && c->n % (64 * T) != 0) T /= 2;
+    c->T = T;
+    c->nstripes = (int)((c->n + 64 * T - 1) / (64 * T));
+    c->nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : c->nstripes <= 4 * c->num_cu ? 4 : 8;
+    c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
 }
 
 int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
@@ -342,9 +372,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
     // one stripe (64 columns) per compute wave; a workgroup (one per CU) chains 4 waves (one per
     // SIMD: the fastest rows) when every stripe gets a wave that way, else 8 (two per SIMD)
-    c->nstripes = (int)((c->n + 63) / 64);
-    c->nwc = c->nstripes <= 4 * c->num_cu ? 4 : 8;
-    c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
+    set_stripes(c, c->T_req, false, false);
     c->h_a.assign(a, a + m);
     c->h_b.assign(b_all, b_all + n_all);
     HIPCHK(c->a.ensure(m));
@@ -373,7 +401,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
         // query-profile ring: as many rows as fit 64 KB (at least 128)
         c->qrows = 1024;
         while (c->qrows > 128 && (size_t)K * c->qrows * c->qbytes > 64 * 1024) c->qrows >>= 1;
-        if (ga::fill_lds_bytes(c->nwc, c->qbytes, K, c->qrows) > 160 * 1024)
+        if (ga::fill_lds_bytes(8, c->qbytes, K, c->qrows) > 160 * 1024)
             return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
     }
     HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
@@ -381,8 +409,6 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
     HIPCHK(c->left.ensure(sizeof(int2) * (m + 1)));
     HIPCHK(c->meta.ensure(sizeof(int) * 8));
-    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
-    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     HIPCHK(c->out_last.ensure(sizeof(int) * 4));
     HIPCHK(c->result.ensure(sizeof(int) * 16));
     HIPCHK(c->ops.ensure(m + n_all + 1024));  // 2-bit levels; the walk flushes whole 128-byte blocks
@@ -401,7 +427,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     const int64_t m = c->m, n = c->n;
     // 16-row chunks; CB 16-byte words per lane per chunk (ga_device.h)
     c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
-    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->TC * 1024));
+    set_stripes(c, c->T_req, tb, full);
+    // traceback words cover T 64-column stripes per fill stripe
+    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
+    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
+    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     if (full) {
         if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
         HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
@@ -442,9 +472,10 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     p.TC = c->TC;
     p.nwc = c->nwc;
     p.qrows = c->qrows;
+    p.cols_per_lane = c->T;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
-    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 4 * c->nstripes));
+    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
@@ -655,6 +686,8 @@ int ga_ctx_create(int device, ga_ctx** out) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             c->num_cu = cus;
+        if (const char* e = getenv("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
+        if (const char* e = getenv("GA_FILL_NWC")) c->nwc_req = atoi(e);
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -860,9 +893,19 @@ int ga_debug_stamps(ga_ctx* c, int enable, unsigned long long* out, int64_t cap)
     if (!c) return fail(GA_E_ARG, "null context");
     c->dbg_on = enable != 0;
     if (out && c->dbg.p) {
-        const int64_t nb = std::min<int64_t>(cap, 4 * (int64_t)c->nstripes);
+        const int64_t nb = std::min<int64_t>(cap, 8 * (int64_t)c->nstripes);
         HIPCHK(hipMemcpy(out, c->dbg.p, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost));
     }
+    return GA_OK;
+}
+
+// Diagnostics: the fill geometry of the loaded problem {T, nstripes, nwc, nslabs}.
+int ga_debug_geometry(ga_ctx* c, int32_t* out4) {
+    if (!c || !out4) return fail(GA_E_ARG, "null argument");
+    out4[0] = c->T;
+    out4[1] = c->nstripes;
+    out4[2] = c->nwc;
+    out4[3] = c->nslabs;
     return GA_OK;
 }
 

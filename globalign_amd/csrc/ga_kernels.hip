@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ga_device.h"
@@ -207,23 +208,6 @@ struct QPack {
     }
 };
 
-// one step of an inclusive prefix-min scan over the wave (DPP; disabled lanes keep INT_MAX)
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ int dpp_min(int x) {
-    return min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, CTRL, ROWMASK, 0xf, false));
-}
-__device__ __forceinline__ int wave_scan_min(int x) {
-    x = dpp_min<0x111, 0xf>(x);  // row_shr:1
-    x = dpp_min<0x112, 0xf>(x);  // row_shr:2
-    x = dpp_min<0x114, 0xf>(x);  // row_shr:4
-    x = dpp_min<0x118, 0xf>(x);  // row_shr:8
-    x = dpp_min<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
-    x = dpp_min<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
-    return x;
-}
-// lane l takes lane l-1's value; lane 0 takes `edge`
-__device__ __forceinline__ int shr1(int edge, int x) { return __builtin_amdgcn_update_dpp(edge, x, 0x138, 0xf, 0xf, false); }
-
 // LDS byte address of a __shared__ object (for hand-issued ds_read)
 template <typename T>
 __device__ __forceinline__ unsigned lds_addr(T* p) {
@@ -262,8 +246,12 @@ __device__ __forceinline__ void lds_publish(unsigned ring_addr, unsigned pc_addr
 enum { CI_PC = 0, CI_PROD0 = 31, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
 constexpr int FILL_CNT_BYTES = 256;
 
-template <int CB, typename QT, bool TB, bool FULL, int NWC>
+template <int CB, typename QT, bool TB, int T>
+__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane);
+
+template <int CB, typename QT, bool TB, bool FULL, int NWC, int T>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
+    static_assert(T == 1 || !FULL, "the FULL debug output is T == 1 only");
     constexpr int W = TbFmt<CB>::W;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -351,7 +339,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                     if (r <= hi) {
                         const int H = rout[r & RMASK].x;
                         g_st64(dst + r, make_int2(H, rout[(r - 1) & RMASK].y + o));
-                        if (last_slab && r == (unsigned)m) p.out_last[0] = H;  // H'(m, n): the cost
+                        if (T == 1 && last_slab && r == (unsigned)m) p.out_last[0] = H;  // H'(m, n): the cost
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) {
@@ -380,6 +368,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         return;
     }
     if (w >= nlive) return;
+    if constexpr (T > 1) {
+        fill_blocked<CB, QT, TB, T>(p, cnt, ring, qring, w, g, lane);
+        return;
+    }
 
     // ---------------- compute wave w: stripe s ----------------
     // compute waves win VALU arbitration against the IO wave on their SIMD (the chain head,
@@ -554,10 +546,177 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     if (lane == srcl) rout[mpad & RMASK].x = Hprev;
     if (lane == 0) __hip_atomic_store(&pc.prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
     if (p.dbg != nullptr && lane == 0) {
-        p.dbg[4 * s] = stamp0;
-        p.dbg[4 * s + 1] = stamp1;
-        p.dbg[4 * s + 2] = __builtin_amdgcn_s_memrealtime();
-        p.dbg[4 * s + 3] = __builtin_amdgcn_s_memtime() - clk0;  // shader clocks from chunk 1 to the end
+        p.dbg[8 * s + 0] = stamp0;
+        p.dbg[8 * s + 1] = stamp1;
+        p.dbg[8 * s + 2] = __builtin_amdgcn_s_memrealtime();
+        p.dbg[8 * s + 3] = __builtin_amdgcn_s_memtime() - clk0;  // shader clocks from chunk 1 to the end
+    }
+}
+
+// ---------------- blocked compute wave: T columns per lane ----------------
+// Stripe s covers columns 64*T*s + 1 .. 64*T*(s+1); lane l owns the T consecutive columns
+// 64*T*s + l*T + 1 .. + T.  One row (the same recurrence as the T == 1 loop above):
+//   M' = H'(i-1, j-1) + sub'           (column 0 of a lane: the left lane's last column, DPP)
+//   U  = min(M', Y')                    per column
+//   P  = in-register prefix-min of U over the lane's T columns
+//   S  = ONE wave scan of the lanes' totals P[T-1] (six DPP steps for 64*T cells)
+//   C  = S of the lane to the left (lane 0: the stripe's left-edge V~), V~ = min(C, P)
+//   X' = V~(j-1) + o,  H' = min(U, X'),  h2' = min(Y', H' + o)
+// so the scan, the edge traffic and the wave-uniform control are paid once per 64*T cells.
+// The stripe's right edge is lane 63's last column; only the stripe holding column n may be
+// partial, and its compute wave writes the cost H'(m, n) itself.  Traceback words keep the
+// 64-column layout of ga_device.h: column (l, k) is lane (l*T + k) % 64 of 64-column stripe
+// T*s + (l*T) / 64, so a lane's T words are one contiguous 16*T-byte run.
+template <int CB, typename QT, bool TB, int T>
+__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane) {
+    constexpr int W = TbFmt<CB>::W;
+    __builtin_amdgcn_s_setprio(2);
+    unsigned* abort_sh = cnt + CI_ABORT;
+    auto prod = [&](int k) -> unsigned* { return k == 0 ? cnt + CI_PROD0 : cnt + 2 * k - 1; };
+    auto cons = [&](int k) -> unsigned* { return cnt + 2 * k; };
+    const int m = p.m, o = p.o, n = p.n;
+    const int nch = (m + FROWS - 1) / FROWS;
+    const int mpad = nch * FROWS;
+    const int QR = p.qrows;
+    const unsigned qmask = (unsigned)QR - 1u;
+    const int s = g * p.nwc + w;
+    const int j0 = s * 64 * T;
+    const int jl = j0 + lane * T;  // this lane: columns jl+1 .. jl+T
+    const QT* qcol[T];
+    int Hprev[T], Yc[T];  // H'(i-1, j), h2'(i-1, j)
+#pragma unroll
+    for (int k = 0; k < T; k++) {
+        const int jc = jl + k + 1;
+        const bool ok = jc <= n;
+        qcol[k] = qring + (ok ? p.b[jc - 1] : 0) * QR;
+        const int2 t = p.top[ok ? jc : n];
+        Hprev[k] = t.x;
+        Yc[k] = t.y;
+    }
+    // the stripe holding column n (the last one) reports H'(m, n) from lane ke_l, column ke_k
+    const bool has_n = j0 < n && n <= j0 + 64 * T;
+    const int ke_l = (n - 1 - j0) / T, ke_k = (n - 1 - j0) % T;
+    int Hm[T];
+#pragma unroll
+    for (int k = 0; k < T; k++) Hm[k] = 0;
+    const unsigned op1 = (unsigned)o + 1u;
+    const int2* rin = ring + w * RING;
+    int2* rout = ring + (w + 1) * RING;
+    uint4* tbw = TB ? reinterpret_cast<uint4*>(p.tb) + ((long long)(T * s + (lane * T) / 64) * p.TC) * 64 + (lane * T) % 64
+                    : nullptr;
+    unsigned avail = 0, outfree = 0, qavail = 0;
+    const unsigned pc_lds = lds_addr(cons(w));  // {cons[w], prod[w + 1]}
+    const unsigned rout_lds = lds_addr(rout);
+    const unsigned long long edgemask = 1ull << 63;
+    bool aborted = false;
+    const bool dbg = p.dbg != nullptr;
+    unsigned long long wcyc[3] = {0, 0, 0}, nsleep = 0, clk0 = 0, stamp0 = 0, stamp1 = 0;
+    // wait (wave-uniform) until *ctr + add >= target; kind: 0 edges in, 1 ring space out, 2 profile
+    auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target, int kind) {
+        unsigned spins = 0;
+        cached = sgpr_u(cached);
+        unsigned long long t0 = 0;
+        if (dbg && (int)cached < target) t0 = __builtin_amdgcn_s_memtime();
+        while ((int)cached < target && !aborted) {
+            cached = lds_ldu(ctr) + add;
+            if ((int)cached >= target) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) aborted = true;
+        }
+        if (dbg && t0) {
+            wcyc[kind] += __builtin_amdgcn_s_memtime() - t0;
+            nsleep += spins;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    };
+    wait_ge(prod(w), 0, avail, 4, 0);
+    int4 e01 = reinterpret_cast<const int4*>(rin)[0];
+    int4 e23 = reinterpret_cast<const int4*>(rin)[1];
+    const unsigned* prod_in = prod(w);
+    unsigned pnext = *prod_in;
+
+    for (int c = 0; c < nch; c++) {
+        const int row0 = __builtin_amdgcn_readfirstlane(c * FROWS);
+        if (dbg && c == 1) {
+            stamp0 = __builtin_amdgcn_s_memrealtime();
+            clk0 = __builtin_amdgcn_s_memtime();
+        }
+        if (dbg && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
+        wait_ge(cons(w + 1), RING, outfree, row0 + FROWS + 1, 1);
+        wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + FROWS, 2);
+        QPack<QT> q[T];
+#pragma unroll
+        for (int k = 0; k < T; k++) q[k].load(qcol[k] + ((unsigned)row0 & qmask));
+        // row m inside this chunk (uniform; -1: none / not the stripe holding column n)
+        const int um = __builtin_amdgcn_readfirstlane((has_n && m - 1 - row0 < FROWS) ? m - 1 - row0 : -1);
+        uint32_t acc[T][4 * CB];
+        if (TB) {
+#pragma unroll
+            for (int k = 0; k < T; k++)
+#pragma unroll
+                for (int d = 0; d < 4 * CB; d++) acc[k][d] = 0;
+        }
+#pragma unroll
+        for (int sc = 0; sc < FROWS / 4; sc++) {
+            const int r0 = __builtin_amdgcn_readfirstlane(row0 + 4 * sc);
+            const int eh[4] = {e01.x, e01.z, e23.x, e23.z};  // H'(i-1, edge)
+            const int ev[4] = {e01.y, e01.w, e23.y, e23.w};  // V~(i, edge)
+            int4 n01, n23;
+            int oH[4], oV[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int uu = 4 * sc + u;
+                int sub[T];
+#pragma unroll
+                for (int k = 0; k < T; k++) sub[k] = q[k].get(uu);
+                blocked_row<T, TB, CB>(Hprev, Yc, eh[u], ev[u], sub, o, op1, uu, acc, oH[u], oV[u]);
+                if (uu == um) {
+#pragma unroll
+                    for (int k = 0; k < T; k++) Hm[k] = Hprev[k];
+                }
+                if (u == 0) {
+                    if (r0 + 4 < mpad) {
+                        avail = sgpr_u(max(avail, pnext));
+                        wait_ge(prod(w), 0, avail, r0 + 8, 0);
+                    }
+                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 4) & RMASK));
+                    n01 = e4[0];
+                    n23 = e4[1];
+                    pnext = *prod_in;
+                }
+            }
+            lds_publish(rout_lds + (unsigned)(r0 & RMASK) * 8u, pc_lds, edgemask, v4i{oH[0], oV[0], oH[1], oV[1]},
+                        v4i{oH[2], oV[2], oH[3], oV[3]}, (unsigned)(r0 + 3), (unsigned)(r0 + 4));
+            e01 = n01;
+            e23 = n23;
+        }
+        if (TB) {
+#pragma unroll
+            for (int d = 0; d < CB; d++)
+#pragma unroll
+                for (int k = 0; k < T; k++)
+                    tbw[d * 64 + k] = make_uint4(acc[k][4 * d], acc[k][4 * d + 1], acc[k][4 * d + 2], acc[k][4 * d + 3]);
+            tbw += CB * 64;
+        }
+    }
+    if (lane == 63) rout[mpad & RMASK].x = Hprev[T - 1];
+    if (lane == 0) __hip_atomic_store(prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
+    if (has_n && lane == ke_l) {
+        int v = Hm[0];
+#pragma unroll
+        for (int k = 1; k < T; k++)
+            if (k == ke_k) v = Hm[k];
+        p.out_last[0] = v;
+    }
+    if (dbg && lane == 0) {
+        unsigned long long* d = p.dbg + 8 * s;
+        d[0] = stamp0;
+        d[1] = stamp1;
+        d[2] = __builtin_amdgcn_s_memrealtime();
+        d[3] = __builtin_amdgcn_s_memtime() - clk0;
+        d[4] = wcyc[0];
+        d[5] = wcyc[1];
+        d[6] = wcyc[2];
+        d[7] = nsleep;
     }
 }
 
@@ -1104,36 +1263,55 @@ size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows) {
     return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * qrows * qbytes;
 }
 
-template <int CB, typename QT, bool TB, bool FULL, int NWC>
+template <int CB, typename QT, bool TB, bool FULL, int NWC, int T>
 static void launch_one(hipStream_t s, const FillArgs& p) {
-    const size_t lds = std::max<size_t>(fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), FILL_LDS_MIN);
-    auto* fn = fill_kernel<CB, QT, TB, FULL, NWC>;
+    // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
+    static const long floor_env = [] {
+        const char* e = getenv("GA_FILL_LDS_FLOOR");
+        return e ? atol(e) : -1L;
+    }();
+    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t lds = std::max<size_t>(fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
+    auto* fn = fill_kernel<CB, QT, TB, FULL, NWC, T>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
 
-template <typename QT, int NWC>
+template <typename QT, int NWC, int T>
 static void launch_fill_t(hipStream_t s, const FillArgs& p, int CB, bool tb, bool full) {
-    if (!tb) return launch_one<1, QT, false, false, NWC>(s, p);
-    if (full) {
-        if (CB == 1) launch_one<1, QT, true, true, NWC>(s, p);
-        else if (CB == 2) launch_one<2, QT, true, true, NWC>(s, p);
-        else launch_one<4, QT, true, true, NWC>(s, p);
-        return;
+    if (!tb) return launch_one<1, QT, false, false, NWC, T>(s, p);
+    if constexpr (T == 8) return;  // score only (the host never asks for it with traceback words)
+    else {
+    if constexpr (T == 1) {
+        if (full) {
+            if (CB == 1) launch_one<1, QT, true, true, NWC, 1>(s, p);
+            else if (CB == 2) launch_one<2, QT, true, true, NWC, 1>(s, p);
+            else launch_one<4, QT, true, true, NWC, 1>(s, p);
+            return;
+        }
     }
-    if (CB == 1) launch_one<1, QT, true, false, NWC>(s, p);
-    else if (CB == 2) launch_one<2, QT, true, false, NWC>(s, p);
-    else launch_one<4, QT, true, false, NWC>(s, p);
+    if (CB == 1) launch_one<1, QT, true, false, NWC, T>(s, p);
+    else if (CB == 2) launch_one<2, QT, true, false, NWC, T>(s, p);
+    else launch_one<4, QT, true, false, NWC, T>(s, p);
+    }
+}
+
+template <int T>
+static void launch_fill_T(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full) {
+    if (p.nwc == 4) {
+        if (qbytes == 1) launch_fill_t<int8_t, 4, T>(s, p, CB, tb, full);
+        else launch_fill_t<int16_t, 4, T>(s, p, CB, tb, full);
+    } else {
+        if (qbytes == 1) launch_fill_t<int8_t, 8, T>(s, p, CB, tb, full);
+        else launch_fill_t<int16_t, 8, T>(s, p, CB, tb, full);
+    }
 }
 
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full) {
-    if (p.nwc == 4) {
-        if (qbytes == 1) launch_fill_t<int8_t, 4>(s, p, CB, tb, full);
-        else launch_fill_t<int16_t, 4>(s, p, CB, tb, full);
-    } else {
-        if (qbytes == 1) launch_fill_t<int8_t, 8>(s, p, CB, tb, full);
-        else launch_fill_t<int16_t, 8>(s, p, CB, tb, full);
-    }
+    if (p.cols_per_lane == 8) launch_fill_T<8>(s, p, CB, qbytes, tb, full);
+    else if (p.cols_per_lane == 4) launch_fill_T<4>(s, p, CB, qbytes, tb, full);
+    else if (p.cols_per_lane == 2) launch_fill_T<2>(s, p, CB, qbytes, tb, full);
+    else launch_fill_T<1>(s, p, CB, qbytes, tb, full);
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {

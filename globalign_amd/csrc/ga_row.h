@@ -64,4 +64,62 @@ __device__ __forceinline__ void row_asm(int Hprev, int Yc, int eh, int ev, uint3
 }
 #undef GA_ROW_ASM
 
+// one step of an inclusive prefix-min scan over the wave (DPP; disabled lanes keep INT_MAX)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_min(int x) {
+    return min(x, __builtin_amdgcn_update_dpp(0x7fffffff, x, CTRL, ROWMASK, 0xf, false));
+}
+__device__ __forceinline__ int wave_scan_min(int x) {
+    x = dpp_min<0x111, 0xf>(x);  // row_shr:1
+    x = dpp_min<0x112, 0xf>(x);  // row_shr:2
+    x = dpp_min<0x114, 0xf>(x);  // row_shr:4
+    x = dpp_min<0x118, 0xf>(x);  // row_shr:8
+    x = dpp_min<0x142, 0xa>(x);  // row_bcast:15 -> rows 1, 3
+    x = dpp_min<0x143, 0xc>(x);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// lane l takes lane l-1's value; lane 0 takes `edge`
+__device__ __forceinline__ int shr1(int edge, int x) { return __builtin_amdgcn_update_dpp(edge, x, 0x138, 0xf, 0xf, false); }
+
+// One row of a blocked stripe (T columns per lane; fill_blocked in ga_kernels.hip):
+//   M' = H'(i-1, j-1) + sub', U = min(M', Y'), P = the lane's prefix-min of U, one wave scan
+//   of the lanes' totals, C = the scan of the lane to the left (lane 0: ev = V~(i, left edge)),
+//   V~ = min(C, P), X' = V~(j-1) + o, H' = min(U, X'), h2' = min(Y', H' + o).
+// Hprev/Yc: H'(i-1, j) / h2'(i-1, j) in, H'(i, j) / h2'(i, j) out; eh = H'(i-1, left edge);
+// oH / oV: what the next stripe needs from this lane's last column (H'(i-1), V~(i)).
+// TB: the cell's traceback code goes into acc[k] at byte uu*CB (W-bit fields, fill_kernel).
+template <int T, bool TB, int CB>
+__device__ __forceinline__ void blocked_row(int (&Hprev)[T], int (&Yc)[T], int eh, int ev, const int (&sub)[T], int o,
+                                            unsigned op1, int uu, uint32_t (&acc)[T][4 * CB], int& oH, int& oV) {
+    constexpr int W = (8 * CB - 1) / 2;
+    int M[T], U[T], P[T];
+    M[0] = shr1(eh, Hprev[T - 1]) + sub[0];
+#pragma unroll
+    for (int k = 1; k < T; k++) M[k] = Hprev[k - 1] + sub[k];
+#pragma unroll
+    for (int k = 0; k < T; k++) U[k] = min(M[k], Yc[k]);
+    P[0] = U[0];
+#pragma unroll
+    for (int k = 1; k < T; k++) P[k] = min(P[k - 1], U[k]);
+    const int Wv = min(wave_scan_min(P[T - 1]), ev);  // V~ at this lane's last column
+    const int C = shr1(ev, Wv);                       // V~ left of this lane's first column
+    oH = Hprev[T - 1];
+    oV = Wv;
+    int Vl = C;
+#pragma unroll
+    for (int k = 0; k < T; k++) {
+        const int X = Vl + o;
+        const int H = min(U[k], X);
+        if (TB) {
+            const unsigned code = min((unsigned)(X - H), op1) | (min((unsigned)(Yc[k] - H), op1) << W) |
+                                  (min((unsigned)(M[k] - H), 1u) << (2 * W));
+            const int pu = uu * CB;
+            acc[k][pu >> 2] |= code << (pu * 8 & 31);
+        }
+        if (k + 1 < T) Vl = min(C, P[k]);
+        Yc[k] = min(Yc[k], H + o);
+        Hprev[k] = H;
+    }
+}
+
 }  // namespace ga

@@ -34,7 +34,7 @@ import time
 import numpy as np
 
 
-def slab_bounds(n, world, align=64):
+def slab_bounds(n, world, align=256):
     """Contiguous column slabs [c_k, c_{k+1}); inner edges on multiples of `align` when n allows."""
     if world < 1 or n < world:
         raise ValueError(f"cannot split {n} columns over {world} ranks")

@@ -26,16 +26,18 @@ L.ga_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
 eng.fill(traceback=tb)
 L.ga_debug_stamps(eng._h, 1, None, 0)
 cost, _ = eng.fill(traceback=tb)
-ns = (n + 63) // 64
-buf = np.zeros(4 * ns, dtype=np.uint64)
+L.ga_debug_geometry.argtypes = [C.c_void_p, C.c_void_p]
+geo = np.zeros(4, dtype=np.int32)
+L.ga_debug_geometry(eng._h, geo.ctypes.data)
+T, ns, nwc = int(geo[0]), int(geo[1]), int(geo[2])
+buf = np.zeros(8 * ns, dtype=np.uint64)
 L.ga_debug_stamps(eng._h, 0, buf.ctypes.data, buf.size)
-st = buf.reshape(ns, 4).astype(np.int64)
+st = buf.reshape(ns, 8).astype(np.int64)
 t0 = st[:, 0].min()
 start, mid, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0, (st[:, 2] - t0) / 100.0  # microseconds
 f_ms = eng.kernel_ms()[0]
 dur = end - start
 step_ns = dur * 1e3 / m
-nwc = 4 if ns <= 4 * 256 else 8  # compute waves per workgroup (ga_host.cpp load_problem)
 out = {
     "m": m, "n": n, "tb": tb, "cost": cost, "fill_kernel_ms": f_ms, "nstripes": ns,
     "last_stripe_start_us": float(start[-1]), "last_end_us": float(end.max()),
@@ -51,6 +53,16 @@ out = {
     "cycles_per_row_median": float(np.median(st[:, 3] / m)),
     "first_stripes_row_ns": [float(x) for x in step_ns[:10]],
     "row_ns_min": float(np.min(step_ns)),
+    "cols_per_lane": T, "nwc": nwc,
+    # blocked stripes (T > 1): shader clocks waiting for edges in / ring space out / the profile
+    "wait_frac_edges_in": float(np.median(st[:, 4] / np.maximum(st[:, 3], 1))),
+    "wait_frac_ring_out": float(np.median(st[:, 5] / np.maximum(st[:, 3], 1))),
+    "wait_frac_profile": float(np.median(st[:, 6] / np.maximum(st[:, 3], 1))),
+    "sleeps_per_row": float(np.median(st[:, 7] / m)),
+    # by position in the workgroup chain: the waves that wait least set the chain's pace
+    "wait_frac_edges_in_by_wave": [round(float(np.median(st[k::nwc, 4] / np.maximum(st[k::nwc, 3], 1))), 3)
+                                   for k in range(nwc)],
+    "cycles_per_row_by_wave": [round(float(np.median(st[k::nwc, 3] / m)), 1) for k in range(nwc)],
 }
 # one align for the walk diagnostics
 import random  # noqa: E402
