@@ -65,5 +65,8 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows);
 void launch_walk(hipStream_t s, const WalkArgs& w);
+// score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)
+void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full);
+size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows);
 
 }  // namespace ga

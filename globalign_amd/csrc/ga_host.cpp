@@ -263,7 +263,9 @@ struct ga_ctx {
     int64_t n_global = 0, col0 = 0;
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
-    int T = 1, T_req = 0, nwc_req = 0;      // columns per lane of the fill (T_req 0: automatic; GA_COLS_PER_LANE)
+    int T = 1, T_req = 0, nwc_req = 0;
+    int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal (GA_FILL_MODE)
+    bool diag = false;         // the last enqueued fill used the anti-diagonal kernel      // columns per lane of the fill (T_req 0: automatic; GA_COLS_PER_LANE)
     int64_t GV_m = 0, GH_n = 0;
     std::vector<uint8_t> h_a, h_b;
     // device buffers
@@ -401,7 +403,8 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
         // query-profile ring: as many rows as fit 64 KB (at least 128)
         c->qrows = 1024;
         while (c->qrows > 128 && (size_t)K * c->qrows * c->qbytes > 64 * 1024) c->qrows >>= 1;
-        if (ga::fill_lds_bytes(8, c->qbytes, K, c->qrows) > 160 * 1024)
+        if (std::max(ga::fill_lds_bytes(8, c->qbytes, K, c->qrows), ga::fill_diag_lds_bytes(8, c->qbytes, K, c->qrows)) >
+            160 * 1024)
             return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
     }
     HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
@@ -427,7 +430,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     const int64_t m = c->m, n = c->n;
     // 16-row chunks; CB 16-byte words per lane per chunk (ga_device.h)
     c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
-    set_stripes(c, c->T_req, tb, full);
+    // score only: the anti-diagonal kernel (64-column stripes) when asked for and its profile
+    // ring is deep enough for a workgroup's skew (8 waves x 64 steps)
+    c->diag = (!tb || (full && c->qbytes == 1 && c->nstripes <= 4 * c->num_cu)) && c->diag_req == 2 && c->qrows >= 1024;
+    set_stripes(c, c->diag ? 1 : c->T_req, tb, full);
+    if (c->diag && full) {  // the debug FULL variant is built for 4 compute waves
+        c->nwc = 4;
+        c->nslabs = (c->nstripes + 3) / 4;
+    }
     // traceback words cover T 64-column stripes per fill stripe
     if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
     HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
@@ -478,7 +488,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    if (c->diag) ga::launch_fill_diag(c->stream, p, c->qbytes, full);
+    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
     c->filled_tb = tb;
@@ -688,6 +699,7 @@ int ga_ctx_create(int device, ga_ctx** out) {
             c->num_cu = cus;
         if (const char* e = getenv("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
         if (const char* e = getenv("GA_FILL_NWC")) c->nwc_req = atoi(e);
+        if (const char* e = getenv("GA_FILL_MODE")) c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : 0;
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;

@@ -202,6 +202,8 @@ struct QPack {
             w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
         }
     }
+    // a lane's rows at any byte offset (the anti-diagonal fill's profile; LDS allows unaligned reads)
+    __device__ __forceinline__ void load_unaligned(const QT* p) { __builtin_memcpy(w, p, sizeof(w)); }
     __device__ __forceinline__ int get(int u) const {
         if (sizeof(QT) == 1) return (int)(int8_t)(w[u >> 2] >> (8 * (u & 3)));
         return (int)(int16_t)(w[u >> 1] >> (16 * (u & 1)));
@@ -569,7 +571,6 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
 // T*s + (l*T) / 64, so a lane's T words are one contiguous 16*T-byte run.
 template <int CB, typename QT, bool TB, int T>
 __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane) {
-    constexpr int W = TbFmt<CB>::W;
     __builtin_amdgcn_s_setprio(2);
     unsigned* abort_sh = cnt + CI_ABORT;
     auto prod = [&](int k) -> unsigned* { return k == 0 ? cnt + CI_PROD0 : cnt + 2 * k - 1; };
@@ -707,6 +708,292 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
             if (k == ke_k) v = Hm[k];
         p.out_last[0] = v;
     }
+    if (dbg && lane == 0) {
+        unsigned long long* d = p.dbg + 8 * s;
+        d[0] = stamp0;
+        d[1] = stamp1;
+        d[2] = __builtin_amdgcn_s_memrealtime();
+        d[3] = __builtin_amdgcn_s_memtime() - clk0;
+        d[4] = wcyc[0];
+        d[5] = wcyc[1];
+        d[6] = wcyc[2];
+        d[7] = nsleep;
+    }
+}
+
+// ----------------------------------------------------------------------------------
+// The anti-diagonal (skewed) score-only fill (dp_array_forward :366-392 without
+// traceback words).  One wave owns a 64-column stripe; lane l owns column 64s+l+1 and
+// at step t works on row i = t - l + 1, so a step is one anti-diagonal of the stripe
+// and the left neighbour's values are one DPP lane shift of the previous step:
+//     M' = H'(i-1, j-1) + sub'        (H' the left lane shifted in a step earlier)
+//     X' = h1'(i, j-1)                (the left lane's h1' of the previous step)
+//     H' = min(M', X', Y'),  h1' = min(X', H' + o),  h2' = min(Y', H' + o)
+// Seven VALU per 64 cells and no per-row scan: the dependent chain of a step is
+// DPP -> min3 -> add -> min.  Lane 0 takes the stripe's left edge (H', h1') of row t+1
+// from the LDS ring (a broadcast read per 4 steps); lane 63 publishes row t-62 of the
+// right edge every 4 steps.  sub' of the lane's row comes from the LDS query profile by
+// one byte read per step (the ring has a 16-row mirror tail so a lane's 16 reads of a
+// chunk never wrap).  Columns past n (the last stripe only) forward their left input,
+// so lane 63 always carries column n of the partial stripe: the right edge and the
+// cost come out of the same ring as for a full stripe.
+constexpr int QMIRROR = 16;
+
+template <typename QT, int NWC, bool FULL, bool DBG>
+__global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    unsigned* cnt = reinterpret_cast<unsigned*>(smem);
+    int2* ring = reinterpret_cast<int2*>(smem + FILL_CNT_BYTES);
+    QT* qring = reinterpret_cast<QT*>(ring + (NWC + 1) * RING);
+    auto prod = [&](int k) -> unsigned* { return k == 0 ? cnt + CI_PROD0 : cnt + 2 * k - 1; };
+    auto cons = [&](int k) -> unsigned* { return cnt + 2 * k; };
+    unsigned* abort_sh = cnt + CI_ABORT;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[CI_SLAB] = atomicAdd(p.ticket, 1u);
+    __syncthreads();
+    const int g = __builtin_amdgcn_readfirstlane((int)cnt[CI_SLAB]);
+    const int m = p.m, o = p.o;
+    const int nsteps = m + 63;                       // lane 63 reaches row m at step m + 62
+    const int nch = (nsteps + FROWS - 1) / FROWS;
+    const unsigned rows_end = (unsigned)(nch * FROWS + 16);  // every row a consumer may ask for
+    const int nlive = min(NWC, p.nstripes - g * NWC);
+    const int QR = p.qrows;                          // ring rows (power of two) + QMIRROR mirror rows
+    const int QS = QR + QMIRROR;                     // per-code stride
+    const unsigned qmask = (unsigned)QR - 1u;
+
+    if (w == NWC) {
+        // ---------------- IO wave: slab edges HBM <-> LDS rings, query profile ----------------
+        const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
+        const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
+        const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
+        const bool src_sc1 = g != 0 || p.left_prog != nullptr;
+        const bool last_slab = g == p.nslabs - 1;
+        int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
+        int2* rin0 = ring;
+        const int2* rout = ring + nlive * RING;
+        const int K = p.K;
+        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
+        while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
+            bool moved = false;
+            if (q_next < (unsigned)m) {
+                // rows the last wave's lane 63 has published (minus its chunk in flight) are free
+                const unsigned pl = lds_ld(prod(nlive));
+                const unsigned space = (pl > 24u ? pl - 24u : 0u) + (unsigned)QR;
+                const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
+                if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
+                    const unsigned r = q_next + 1 + lane;
+                    if (r <= hi) {
+                        const int x = p.a[r - 1];
+                        const int* sp = p.subp + x * K;
+                        const unsigned slot = (r - 1) & qmask;
+                        QT* qd = qring + slot;
+                        for (int c = 0; c < K; c++) qd[c * QS] = (QT)sp[c];
+                        if (slot < (unsigned)QMIRROR)
+                            for (int c = 0; c < K; c++) qd[c * QS + QR] = (QT)sp[c];
+                    }
+                    if (lane == 0) lds_st(&cnt[CI_PRODQ], hi == (unsigned)m ? rows_end : hi);
+                    q_next = hi;
+                    moved = true;
+                }
+            }
+            if (in_next < (unsigned)m) {
+                const unsigned space = lds_ld(cons(0)) + RING;
+                const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
+                const unsigned hi = min(min(space, avail), in_next + 64);
+                if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
+                    const unsigned r = in_next + 1 + lane;
+                    if (r <= hi) rin0[(r - 1) & RMASK] = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
+                    // rows past m are padding (garbage only rows past m read)
+                    if (lane == 0) lds_st(prod(0), hi == (unsigned)m ? rows_end : hi);
+                    in_next = hi;
+                    moved = true;
+                }
+            }
+            if (out_next < (unsigned)m) {
+                const unsigned P = lds_ld(prod(nlive));
+                const unsigned hi = min(min(P, (unsigned)m), out_next + 64);
+                if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
+                    const unsigned r = out_next + 1 + lane;
+                    if (r <= hi) {
+                        const int2 e = rout[(r - 1) & RMASK];
+                        g_st64(dst + r, e);
+                        if (last_slab && r == (unsigned)m) p.out_last[0] = e.x;  // H'(m, n): the cost
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) {
+                        g_st(p.hand_prog + g, hi);
+                        if (p.edge_prog != nullptr && last_slab)
+                            __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
+                        lds_st(cons(nlive), hi);
+                    }
+                    out_next = hi;
+                    moved = true;
+                }
+            }
+            if (!moved) {
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) {
+                    g_st(p.abort_word, 1u);
+                    break;
+                }
+                if (!spin_ok(spins, limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
+            } else {
+                spins = 0;
+            }
+        }
+        return;
+    }
+    if (w >= nlive) return;
+
+    // ---------------- compute wave w: stripe s ----------------
+    __builtin_amdgcn_s_setprio(2);
+    const int s = g * NWC + w;
+    const int j0 = s * 64;
+    const int jcol = j0 + lane + 1;
+    const bool colok = jcol <= p.n;
+    const bool partial = j0 + 64 > p.n;  // uniform: the stripe holding column n, when it is not whole
+    const int bcode = colok ? p.b[jcol - 1] : 0;
+    const QT* qcol = qring + bcode * QS;
+    int Hout = p.top[colok ? jcol : p.n].x;       // H'(i-1, j) before row i: H'(0, j)
+    int Yc = p.top[colok ? jcol : p.n].y;         // h2'(0, j)
+    int Hd = p.top[colok ? jcol - 1 : p.n].x;     // H'(0, j-1): the diagonal of row 1
+    int Xout = 0;
+    const unsigned rout_lds = lds_addr(ring + (w + 1) * RING);
+    const unsigned pc_lds = lds_addr(cons(w));  // {cons[w], prod[w + 1]}
+    const unsigned long long edgemask = 1ull << 63;
+    unsigned avail = 0, outfree = 0, qavail = 0;
+    bool aborted = false;
+    constexpr bool dbg = DBG;  // timestamps (s_memtime shares lgkmcnt with LDS reads: off the hot path)
+    unsigned long long wcyc[3] = {0, 0, 0}, nsleep = 0, clk0 = 0, stamp0 = 0, stamp1 = 0;
+    auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target, int kind) {
+        unsigned spins = 0;
+        cached = sgpr_u(cached);
+        unsigned long long t0 = 0;
+        if (dbg && (int)cached < target) t0 = __builtin_amdgcn_s_memtime();
+        while ((int)cached < target && !aborted) {
+            cached = lds_ldu(ctr) + add;
+            if ((int)cached >= target) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) aborted = true;
+        }
+        if (dbg && t0) {
+            wcyc[kind] += __builtin_amdgcn_s_memtime() - t0;
+            nsleep += spins;
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    };
+    const int2* rin = ring + w * RING;
+    // slot (r - 1) & RMASK of a ring holds (H', h1') of row r.  Edges are read two sub-chunks
+    // (8 steps) ahead and the profile one chunk ahead: a step is ~30 cycles, an LDS read ~100+.
+    wait_ge(prod(w), 0, avail, 8, 0);
+    int4 e01 = reinterpret_cast<const int4*>(rin)[0];  // rows 1..4 (sub-chunk 0)
+    int4 e23 = reinterpret_cast<const int4*>(rin)[1];
+    int4 f01 = reinterpret_cast<const int4*>(rin)[2];  // rows 5..8 (sub-chunk 1)
+    int4 f23 = reinterpret_cast<const int4*>(rin)[3];
+    int cH = 0, cX = 0;  // lane 63's (H', h1') of the last step of the previous sub-chunk
+    // this lane's 16 profile values of chunk 0: rows 1-l .. 16-l (never wrap: mirror tail)
+    wait_ge(&cnt[CI_PRODQ], 0, qavail, FROWS, 2);
+    QPack<QT> sub;
+    sub.load_unaligned(qcol + (((unsigned)(-lane)) & qmask));
+
+    auto step = [&](int eh, int ex, int sub, bool masked, int t) {
+        const int HL = __builtin_amdgcn_update_dpp(eh, Hout, 0x138, 0xf, 0xf, false);  // wave_shr:1, lane 0: edge
+        const int XL = __builtin_amdgcn_update_dpp(ex, Xout, 0x138, 0xf, 0xf, false);
+        const int M = Hd + sub;
+        Hd = HL;
+        if (!masked) {
+            const int H = min(min(M, XL), Yc);
+            const int Ho = H + o;
+            Xout = min(XL, Ho);
+            Yc = min(Yc, Ho);
+            Hout = H;
+        } else {
+            const int i = t - lane + 1;
+            if (!colok) {  // columns past n forward their left input
+                Hout = HL;
+                Xout = XL;
+            } else if (i >= 1) {
+                const int H = min(min(M, XL), Yc);
+                const int Ho = H + o;
+                if (FULL && i <= m) {
+                    int* f = p.full + 3 * ((long long)i * (p.n + 1) + jcol);
+                    f[0] = M; f[1] = XL; f[2] = Yc;
+                }
+                Xout = min(XL, Ho);
+                Yc = min(Yc, Ho);
+                Hout = H;
+            }
+        }
+    };
+
+    for (int c = 0; c < nch; c++) {
+        const int t0 = __builtin_amdgcn_readfirstlane(c * FROWS);
+        if (dbg && c == 1) {
+            stamp0 = __builtin_amdgcn_s_memrealtime();
+            clk0 = __builtin_amdgcn_s_memtime();
+        }
+        if (dbg && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
+        // ring slots of the rows this chunk publishes (t0-63 .. t0-48) must be free
+        wait_ge(cons(w + 1), RING, outfree, t0 - 47, 1);
+        // the next chunk's profile values (rows up to t0+32 for lane 0)
+        wait_ge(&cnt[CI_PRODQ], 0, qavail, t0 + 2 * FROWS, 2);
+        QPack<QT> subn;
+        subn.load_unaligned(qcol + (((unsigned)(t0 + FROWS - lane)) & qmask));
+        auto sub_chunks = [&](auto MASKED) {
+            constexpr bool MK = decltype(MASKED)::value;
+#pragma unroll
+            for (int sc = 0; sc < FROWS / 4; sc++) {
+                const int r0 = __builtin_amdgcn_readfirstlane(t0 + 4 * sc);  // steps r0 .. r0+3: lane 0 rows r0+1 .. r0+4
+                int eh[4] = {e01.x, e01.z, e23.x, e23.z};
+                int ex[4] = {e01.y, e01.w, e23.y, e23.w};
+                int4 n01, n23;
+                int oH[4], oX[4];
+                // left edges two sub-chunks ahead: rows r0+9 .. r0+12 (slots r0+8 .. r0+11)
+                wait_ge(prod(w), 0, avail, r0 + 12, 0);
+                {
+                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 8) & RMASK));
+                    n01 = e4[0];
+                    n23 = e4[1];
+                }
+                if constexpr (!MK) {
+                    constexpr int QB = (int)sizeof(QT);
+                    diag4_asm<QB == 2>(eh, ex, Hd, Hout, Xout, Yc, sub.w[(4 * sc * QB) >> 2],
+                                       sub.w[((4 * sc + 2) * QB) >> 2], o, oH, oX);
+                    Hd = eh[3];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        step(eh[u], ex[u], sub.get(4 * sc + u), true, r0 + u);
+                        oH[u] = Hout;
+                        oX[u] = Xout;
+                    }
+                }
+                // lane 63 has rows r0-62 .. r0-59; it publishes the 4-slot-aligned group r0-63 .. r0-60
+                // (the first from the previous sub-chunk) so a group never straddles the ring's end;
+                // rows < 1 land in slots nobody reads before their real rows overwrite them
+                const int pr = r0 - 63;
+                lds_publish(rout_lds + (unsigned)((pr - 1) & RMASK) * 8u, pc_lds, edgemask,
+                            v4i{cH, cX, oH[0], oX[0]}, v4i{oH[1], oX[1], oH[2], oX[2]}, (unsigned)(r0 + 4),
+                            (unsigned)max(pr + 3, 0));
+                cH = oH[3];
+                cX = oX[3];
+                e01 = f01;
+                e23 = f23;
+                f01 = n01;
+                f23 = n23;
+            }
+        };
+        if (FULL || partial || t0 < 64) sub_chunks(std::true_type{});
+        else sub_chunks(std::false_type{});
+        sub = subn;
+    }
+    // the last row lane 63 computed (row nch*16 - 63), then everything (rows past m are padding)
+    if (lane == 63) (ring + (w + 1) * RING)[(nch * FROWS - 64) & RMASK] = make_int2(cH, cX);
+    if (lane == 0) __hip_atomic_store(prod(w + 1), rows_end, RLX, WGS);
     if (dbg && lane == 0) {
         unsigned long long* d = p.dbg + 8 * s;
         d[0] = stamp0;
@@ -1312,6 +1599,35 @@ void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, 
     else if (p.cols_per_lane == 4) launch_fill_T<4>(s, p, CB, qbytes, tb, full);
     else if (p.cols_per_lane == 2) launch_fill_T<2>(s, p, CB, qbytes, tb, full);
     else launch_fill_T<1>(s, p, CB, qbytes, tb, full);
+}
+
+size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows) {
+    return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + QMIRROR) * qbytes;
+}
+
+template <typename QT, int NWC, bool FULL, bool DBG = false>
+static void launch_diag_one(hipStream_t s, const FillArgs& p) {
+    if (!DBG && p.dbg != nullptr) return launch_diag_one<QT, NWC, FULL, true>(s, p);
+    static const long floor_env = [] {
+        const char* e = getenv("GA_FILL_LDS_FLOOR");
+        return e ? atol(e) : -1L;
+    }();
+    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t lds = std::max<size_t>(fill_diag_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
+    auto* fn = fill_diag_kernel<QT, NWC, FULL, DBG>;
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+}
+
+void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full) {
+    if (full) return launch_diag_one<int8_t, 4, true>(s, p);  // debug (the host allows int8 profiles only)
+    if (p.nwc == 4) {
+        if (qbytes == 1) launch_diag_one<int8_t, 4, false>(s, p);
+        else launch_diag_one<int16_t, 4, false>(s, p);
+    } else {
+        if (qbytes == 1) launch_diag_one<int8_t, 8, false>(s, p);
+        else launch_diag_one<int16_t, 8, false>(s, p);
+    }
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {

@@ -122,4 +122,64 @@ __device__ __forceinline__ void blocked_row(int (&Hprev)[T], int (&Yc)[T], int e
     }
 }
 
+
+// Four steps of the anti-diagonal fill (fill_diag_kernel), hand-scheduled: per step two DPP
+// lane shifts (the left lane's H' and h1' of the previous step; lane 0 keeps the stripe's
+// left edge that is already in the register), M' = H'(diag) + sub' (SDWA byte/word of the
+// profile dword), H' = min3, h1' and h2' = min(., H' + o).  A DPP source is always written
+// >= 2 VALU ops earlier (the gfx950 DPP read hazard), so no s_nop is needed.
+//   eh[u], ex[u]: in: the edge (H', h1') of step u's row in lane 0; out: HL / XL of step u
+//   Hd: H'(i-1, j-1) of step 0 (in) -> of the next sub-chunk's step 0 (out: eh[3])
+//   H, X: the previous step's H' / h1' (in) -> step 3's (out); oH/oX: every step's
+#define GA_DIAG_STEP(EH, EX, HD, HIN, XIN, QV, SEL, OH, OX)                                          \
+    "v_mov_b32_dpp " EH ", " HIN " wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"                         \
+    "v_mov_b32_dpp " EX ", " XIN " wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"                         \
+    "v_add_u32_sdwa %[M], sext(" QV "), " HD " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:" SEL " src1_sel:DWORD\n\t" \
+    "v_min3_i32 " OH ", %[M], " EX ", %[Y]\n\t"                                                       \
+    "v_add_u32 %[Ho], " OH ", %[o]\n\t"                                                               \
+    "v_min_i32 " OX ", " EX ", %[Ho]\n\t"                                                             \
+    "v_min_i32 %[Y], %[Y], %[Ho]\n\t"
+// step 0 of a block: its M' first and one wait state, so the DPPs are clear of whatever VALU
+// op the compiler placed just before the block (e.g. a copy into H or X)
+#define GA_DIAG_STEP0(EH, EX, HD, HIN, XIN, QV, SEL, OH, OX)                                         \
+    "v_add_u32_sdwa %[M], sext(" QV "), " HD " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:" SEL " src1_sel:DWORD\n\t" \
+    "s_nop 0\n\t"                                                                                   \
+    "v_mov_b32_dpp " EH ", " HIN " wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"                         \
+    "v_mov_b32_dpp " EX ", " XIN " wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"                         \
+    "v_min3_i32 " OH ", %[M], " EX ", %[Y]\n\t"                                                       \
+    "v_add_u32 %[Ho], " OH ", %[o]\n\t"                                                               \
+    "v_min_i32 " OX ", " EX ", %[Ho]\n\t"                                                             \
+    "v_min_i32 %[Y], %[Y], %[Ho]\n\t"
+
+template <bool Q16>
+__device__ __forceinline__ void diag4_asm(int (&eh)[4], int (&ex)[4], int Hd, int& H, int& X, int& Y, uint32_t q0,
+                                          uint32_t q1, int o, int (&oH)[4], int (&oX)[4]) {
+    int M, Ho;
+    if (!Q16) {
+        asm volatile(GA_DIAG_STEP0("%[e0]", "%[x0]", "%[Hd]", "%[H]", "%[X]", "%[q0]", "BYTE_0", "%[h0]", "%[y0]")
+                     GA_DIAG_STEP("%[e1]", "%[x1]", "%[e0]", "%[h0]", "%[y0]", "%[q0]", "BYTE_1", "%[h1]", "%[y1]")
+                     GA_DIAG_STEP("%[e2]", "%[x2]", "%[e1]", "%[h1]", "%[y1]", "%[q0]", "BYTE_2", "%[h2]", "%[y2]")
+                     GA_DIAG_STEP("%[e3]", "%[x3]", "%[e2]", "%[h2]", "%[y2]", "%[q0]", "BYTE_3", "%[h3]", "%[y3]")
+                     : [e0] "+v"(eh[0]), [e1] "+v"(eh[1]), [e2] "+v"(eh[2]), [e3] "+v"(eh[3]), [x0] "+v"(ex[0]),
+                       [x1] "+v"(ex[1]), [x2] "+v"(ex[2]), [x3] "+v"(ex[3]), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
+                       [h2] "=&v"(oH[2]), [h3] "=&v"(oH[3]), [y0] "=&v"(oX[0]), [y1] "=&v"(oX[1]), [y2] "=&v"(oX[2]),
+                       [y3] "=&v"(oX[3]), [Y] "+v"(Y), [M] "=&v"(M), [Ho] "=&v"(Ho)
+                     : [Hd] "v"(Hd), [H] "v"(H), [X] "v"(X), [q0] "v"(q0), [o] "s"(o));
+    } else {
+        asm volatile(GA_DIAG_STEP0("%[e0]", "%[x0]", "%[Hd]", "%[H]", "%[X]", "%[q0]", "WORD_0", "%[h0]", "%[y0]")
+                     GA_DIAG_STEP("%[e1]", "%[x1]", "%[e0]", "%[h0]", "%[y0]", "%[q0]", "WORD_1", "%[h1]", "%[y1]")
+                     GA_DIAG_STEP("%[e2]", "%[x2]", "%[e1]", "%[h1]", "%[y1]", "%[q1]", "WORD_0", "%[h2]", "%[y2]")
+                     GA_DIAG_STEP("%[e3]", "%[x3]", "%[e2]", "%[h2]", "%[y2]", "%[q1]", "WORD_1", "%[h3]", "%[y3]")
+                     : [e0] "+v"(eh[0]), [e1] "+v"(eh[1]), [e2] "+v"(eh[2]), [e3] "+v"(eh[3]), [x0] "+v"(ex[0]),
+                       [x1] "+v"(ex[1]), [x2] "+v"(ex[2]), [x3] "+v"(ex[3]), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
+                       [h2] "=&v"(oH[2]), [h3] "=&v"(oH[3]), [y0] "=&v"(oX[0]), [y1] "=&v"(oX[1]), [y2] "=&v"(oX[2]),
+                       [y3] "=&v"(oX[3]), [Y] "+v"(Y), [M] "=&v"(M), [Ho] "=&v"(Ho)
+                     : [Hd] "v"(Hd), [H] "v"(H), [X] "v"(X), [q0] "v"(q0), [q1] "v"(q1), [o] "s"(o));
+    }
+    H = oH[3];
+    X = oX[3];
+}
+#undef GA_DIAG_STEP
+#undef GA_DIAG_STEP0
+
 }  // namespace ga
