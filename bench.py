@@ -157,17 +157,43 @@ def measure_single(wl, steps, warmup):
                 rng_ms=float(np.mean(rng_ms)))
 
 
-def roofline(wl, fill_ms, traffic):
+# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per 4 cycles per SIMD at the
+# single rate of v_min_i32 / DPP / VOP3 (tools/micro/valu_rate.hip; adds and logic ops dual-issue at 2 per 4)
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
+
+
+def load_valu(name):
+    """Measured fill-kernel wave-instructions per launch from a committed SQ counter summary (profiles/)."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("sq_insts_valu_per_launch")
+    except Exception:
+        return None
+
+
+def roofline(wl, fill_ms, traffic, valu_insts=None):
+    """The HBM roofline of SURVEY 8(d) (algorithmic bytes per cell) plus what actually bounds the kernel:
+    it moves ~1 B/cell or less (traffic, PMC) and is VALU-issue bound, so the VALU issue rate is reported
+    against the single-rate wave-instruction peak beside it."""
     bpc = BYTES_PER_CELL_TB if wl["traceback"] else BYTES_PER_CELL
     cells = wl["m"] * wl["n"]
     achieved = bpc * cells / (fill_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic, "kernel": "fill_kernel", "bytes_per_cell": bpc,
-            "units_per_launch": f"{cells} cells (m*n)", "kernel_ms": fill_ms,
-            "measured_hbm_GBps": (traffic / (fill_ms * 1e-3) / 1e9) if traffic else None}
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "traffic": traffic, "kernel": "fill_kernel", "bytes_per_cell": bpc,
+           "units_per_launch": f"{cells} cells (m*n)", "kernel_ms": fill_ms,
+           "measured_hbm_GBps": (traffic / (fill_ms * 1e-3) / 1e9) if traffic else None}
+    if valu_insts:
+        rate = valu_insts / (fill_ms * 1e-3)
+        out["valu"] = {"insts_per_launch": valu_insts, "insts_per_cell": valu_insts / cells,
+                       "issue_rate": rate, "peak_single_rate": VALU_PEAK_INSTS, "frac": rate / VALU_PEAK_INSTS,
+                       "unit": "wave64 instructions/s", "source": "SQ_INSTS_VALU (profiles/valu_<workload>.json)"}
+    return out
 
 
 TRAFFIC_FILES = {"c3": "traffic.json", "c4": "traffic_c4.json"}
+VALU_FILES = {"c3": "valu_c3.json", "c4": "valu_c4.json"}
 
 
 def main():
@@ -203,7 +229,8 @@ def main():
         "config": {"workload": wl["desc"], "m": wl["m"], "n": wl["n"], "traceback": wl["traceback"],
                    "parallelism": "single GPU", "cost": r["cost"], "oracle_cost": gold,
                    "cost_matches_oracle": (r["cost"] == gold) if gold is not None else None},
-        "roofline": roofline(wl, r["fill_ms"], load_traffic(TRAFFIC_FILES.get(args.workload, "none.json"))),
+        "roofline": roofline(wl, r["fill_ms"], load_traffic(TRAFFIC_FILES.get(args.workload, "none.json")),
+                             load_valu(VALU_FILES.get(args.workload, "none.json"))),
         "fill_cells_per_s": r["cells"] / (r["fill_ms"] * 1e-3),
     }
     if wl["traceback"]:
@@ -216,7 +243,8 @@ def main():
         line["headline_c3"] = {"workload": w3["desc"], "value": h["value"], "unit": "cells/s",
                                "ms_per_step": h["ms_per_step"], "cost": h["cost"], "fill_ms": h["fill_ms"],
                                "walk_ms": h["walk_ms"], "host_tiebreak_ms": h["rng_ms"],
-                               "roofline": roofline(w3, h["fill_ms"], load_traffic("traffic.json"))}
+                               "roofline": roofline(w3, h["fill_ms"], load_traffic("traffic.json"),
+                                                    load_valu("valu_c3.json"))}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, traceback=wl["traceback"])
     print(json.dumps(line))

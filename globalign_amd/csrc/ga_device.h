@@ -61,7 +61,8 @@ struct WalkArgs {
 
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,
                      int o, int big, int* GVp, int* GHp, int2* top, int2* left, int* bnd_row, int* bnd_col, int* meta,
-                     bool custom);
+                     bool custom, int* scratch);
+int boundary_scratch_ints(int m, int n);  // ints of scratch launch_boundary needs
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows);
 void launch_walk(hipStream_t s, const WalkArgs& w);

@@ -269,7 +269,7 @@ struct ga_ctx {
     int64_t GV_m = 0, GH_n = 0;
     std::vector<uint8_t> h_a, h_b;
     // device buffers
-    DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng,
+    DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng, bscr,
         ops, result;
     DevBuf halo_in{nullptr, 0, true};
     bool slab = false;
@@ -408,6 +408,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
             return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
     }
     HIPCHK(c->GVp.ensure(sizeof(int) * (m + 1)));
+    HIPCHK(c->bscr.ensure(sizeof(int) * ga::boundary_scratch_ints((int)m, (int)n_all)));
     HIPCHK(c->GHp.ensure(sizeof(int) * (n_all + 1)));
     HIPCHK(c->top.ensure(sizeof(int2) * (n_all + 1)));
     HIPCHK(c->left.ensure(sizeof(int2) * (m + 1)));
@@ -451,7 +452,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
     ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
                         c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
-                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom);
+                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom,
+                        c->bscr.as<int>());
     ga::FillArgs p{};
     p.a = c->a.as<uint8_t>();
     p.subp = c->qp.as<int>();
@@ -721,7 +723,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
-                      &c->result, &c->halo_in, &c->dbg, &c->wdbg})
+                      &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& e : c->ev)

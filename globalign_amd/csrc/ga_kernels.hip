@@ -141,6 +141,120 @@ __global__ void __launch_bounds__(1024) boundary_kernel(const uint8_t* __restric
     if (threadIdx.x == 0) { meta[0] = GVp[m]; meta[1] = GHp[n]; }
 }
 
+// The same boundary with the prefix sums spread over the chip (the single-workgroup scan
+// above is latency-bound: ~5 ms at 10^6 columns).  Segments of BSEG codes per workgroup:
+// bnd_sums (segment sums) -> bnd_scan (one workgroup scans the segment sums) -> bnd_apply
+// (each segment rescans itself from its base) -> bnd_edges (elementwise boundary values).
+constexpr int BSEG = 4096;  // 256 threads x 16 consecutive codes
+__global__ void __launch_bounds__(256) bnd_sums_kernel(const uint8_t* __restrict__ a, int m, const uint8_t* __restrict__ b,
+                                                       int n, const int* __restrict__ gh, const int* __restrict__ gv,
+                                                       int nba, int* __restrict__ bs) {
+    __shared__ int red[256];
+    const int k = blockIdx.x;
+    const bool isa = k < nba;
+    const uint8_t* sq = isa ? a : b;
+    const int* g = isa ? gv : gh;
+    const int len = isa ? m : n;
+    const int lo = (isa ? k : k - nba) * BSEG;
+    int acc = 0;
+    for (int q = lo + threadIdx.x; q < min(len, lo + BSEG); q += 256) acc += g[sq[q]];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bs[k] = red[0];
+}
+
+// exclusive scan, in place, of bs[0, nba) and of bs[nba, nba + nbb) (one workgroup)
+__global__ void __launch_bounds__(1024) bnd_scan_kernel(int* __restrict__ bs, int nba, int nbb) {
+    __shared__ int sh[1024];
+    for (int part = 0; part < 2; part++) {
+        int* v = part == 0 ? bs : bs + nba;
+        const int len = part == 0 ? nba : nbb;
+        int carry = 0;
+        for (int base = 0; base < len; base += 1024) {
+            const int q = base + (int)threadIdx.x;
+            const int x = q < len ? v[q] : 0;
+            sh[threadIdx.x] = x;
+            __syncthreads();
+            for (int off = 1; off < 1024; off <<= 1) {
+                const int y = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+                __syncthreads();
+                sh[threadIdx.x] += y;
+                __syncthreads();
+            }
+            if (q < len) v[q] = carry + sh[threadIdx.x] - x;
+            carry += sh[1023];
+            __syncthreads();
+        }
+    }
+}
+
+// pre[q] = sum of g over codes < q, for the segment's q; the last segment also writes pre[len]
+__global__ void __launch_bounds__(256) bnd_apply_kernel(const uint8_t* __restrict__ a, int m, const uint8_t* __restrict__ b,
+                                                        int n, const int* __restrict__ gh, const int* __restrict__ gv,
+                                                        int nba, const int* __restrict__ bs, int* __restrict__ GVp,
+                                                        int* __restrict__ GHp) {
+    __shared__ int sh[256];
+    const int k = blockIdx.x;
+    const bool isa = k < nba;
+    const uint8_t* sq = isa ? a : b;
+    const int* g = isa ? gv : gh;
+    int* pre = isa ? GVp : GHp;
+    const int len = isa ? m : n;
+    const int lo = (isa ? k : k - nba) * BSEG + 16 * (int)threadIdx.x;
+    int v[16];
+    int acc = 0;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        v[u] = lo + u < len ? g[sq[lo + u]] : 0;
+        acc += v[u];
+    }
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const int y = (int)threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += y;
+        __syncthreads();
+    }
+    int run = bs[k] + sh[threadIdx.x] - acc;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+        if (lo + u < len) pre[lo + u] = run;
+        run += v[u];
+        if (lo + u == len - 1) pre[len] = run;
+    }
+}
+
+__global__ void __launch_bounds__(256) bnd_edges_kernel(int m, int n, int o, int big, const int* __restrict__ GVp,
+                                                        const int* __restrict__ GHp, int2* __restrict__ top,
+                                                        int2* __restrict__ left, int* __restrict__ bnd_row,
+                                                        int* __restrict__ bnd_col, int* __restrict__ meta) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t <= n) {
+        const int j = t;
+        int M, X, Y;
+        if (j == 0) { M = X = Y = 0; }                        // :778
+        else { M = big; X = o + GHp[j]; Y = big; }            // :780-784, :802-809
+        bnd_row[3 * j] = M; bnd_row[3 * j + 1] = X; bnd_row[3 * j + 2] = Y;
+        const int H = min(min(M, X), Y);
+        top[j] = make_int2(H - GHp[j], min(Y, H + o) - GHp[j]);
+    }
+    if (t <= m) {
+        const int i = t;
+        int M, X, Y;
+        if (i == 0) { M = X = Y = 0; }
+        else { M = big; X = big; Y = o + GVp[i]; }            // :789-793, :812-819
+        bnd_col[3 * i] = M; bnd_col[3 * i + 1] = X; bnd_col[3 * i + 2] = Y;
+        const int H = min(min(M, X), Y);
+        left[i] = make_int2(H - GVp[i], min(X, H + o) - GVp[i]);
+    }
+    if (t == 0) { meta[0] = GVp[m]; meta[1] = GHp[n]; }
+}
+
 // Custom boundary triples (host supplied, original space) -> shifted edges.
 __global__ void custom_boundary_kernel(const uint8_t* __restrict__ a, int m, const uint8_t* __restrict__ b, int n,
                                        const int* __restrict__ gh, const int* __restrict__ gv, int o,
@@ -248,10 +362,12 @@ __device__ __forceinline__ void lds_publish(unsigned ring_addr, unsigned pc_addr
 enum { CI_PC = 0, CI_PROD0 = 31, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
 constexpr int FILL_CNT_BYTES = 256;
 
-template <int CB, typename QT, bool TB, int T>
+template <int CB, typename QT, bool TB, int T, bool DBG>
 __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane);
 
-template <int CB, typename QT, bool TB, bool FULL, int NWC, int T>
+// DBG: per-stripe timestamps into p.dbg (s_memtime shares lgkmcnt with LDS reads, so the
+// timing code stays out of the production variants)
+template <int CB, typename QT, bool TB, bool FULL, int NWC, int T, bool DBG>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     static_assert(T == 1 || !FULL, "the FULL debug output is T == 1 only");
     constexpr int W = TbFmt<CB>::W;
@@ -309,7 +425,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                         QT* qd = qring + ((r - 1) & qmask);
                         for (int c = 0; c < K; c++) qd[c * QR] = (QT)sp[c];
                     }
-                    if (lane == 0) lds_st(&cnt[CI_PRODQ], hi == (unsigned)m ? (unsigned)mpad : hi);
+                    // done: past the padded rows (the blocked waves read one chunk ahead)
+                    if (lane == 0) lds_st(&cnt[CI_PRODQ], hi == (unsigned)m ? (unsigned)(mpad + FROWS) : hi);
                     q_next = hi;
                     moved = true;
                 }
@@ -371,7 +488,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     }
     if (w >= nlive) return;
     if constexpr (T > 1) {
-        fill_blocked<CB, QT, TB, T>(p, cnt, ring, qring, w, g, lane);
+        fill_blocked<CB, QT, TB, T, DBG>(p, cnt, ring, qring, w, g, lane);
         return;
     }
 
@@ -445,11 +562,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
 
     for (int c = 0; c < nch; c++) {
         const int row0 = __builtin_amdgcn_readfirstlane(c * FROWS);
-        if (p.dbg != nullptr && c == 1) {
+        if (DBG && c == 1) {
             stamp0 = __builtin_amdgcn_s_memrealtime();
             clk0 = __builtin_amdgcn_s_memtime();
         }
-        if (p.dbg != nullptr && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
+        if (DBG && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
         // output ring slots row0 .. row0+FROWS (the tail write included) must be free
         wait_ge(&pc.cons(w + 1), RING, outfree, row0 + FROWS + 1);
         wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + FROWS);
@@ -547,7 +664,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     // H' of the last (padded) row, for the reader's hand-off of row m when m == mpad
     if (lane == srcl) rout[mpad & RMASK].x = Hprev;
     if (lane == 0) __hip_atomic_store(&pc.prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
-    if (p.dbg != nullptr && lane == 0) {
+    if (DBG && lane == 0) {
         p.dbg[8 * s + 0] = stamp0;
         p.dbg[8 * s + 1] = stamp1;
         p.dbg[8 * s + 2] = __builtin_amdgcn_s_memrealtime();
@@ -569,7 +686,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
 // partial, and its compute wave writes the cost H'(m, n) itself.  Traceback words keep the
 // 64-column layout of ga_device.h: column (l, k) is lane (l*T + k) % 64 of 64-column stripe
 // T*s + (l*T) / 64, so a lane's T words are one contiguous 16*T-byte run.
-template <int CB, typename QT, bool TB, int T>
+template <int CB, typename QT, bool TB, int T, bool DBG>
 __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane) {
     __builtin_amdgcn_s_setprio(2);
     unsigned* abort_sh = cnt + CI_ABORT;
@@ -610,7 +727,7 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
     const unsigned rout_lds = lds_addr(rout);
     const unsigned long long edgemask = 1ull << 63;
     bool aborted = false;
-    const bool dbg = p.dbg != nullptr;
+    constexpr bool dbg = DBG;
     unsigned long long wcyc[3] = {0, 0, 0}, nsleep = 0, clk0 = 0, stamp0 = 0, stamp1 = 0;
     // wait (wave-uniform) until *ctr + add >= target; kind: 0 edges in, 1 ring space out, 2 profile
     auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target, int kind) {
@@ -634,6 +751,11 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
     int4 e23 = reinterpret_cast<const int4*>(rin)[1];
     const unsigned* prod_in = prod(w);
     unsigned pnext = *prod_in;
+    // the profile is read one chunk ahead (its LDS latency is off the row chain)
+    wait_ge(&cnt[CI_PRODQ], 0, qavail, FROWS, 2);
+    QPack<QT> q[T];
+#pragma unroll
+    for (int k = 0; k < T; k++) q[k].load(qcol[k]);
 
     for (int c = 0; c < nch; c++) {
         const int row0 = __builtin_amdgcn_readfirstlane(c * FROWS);
@@ -643,10 +765,10 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
         }
         if (dbg && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
         wait_ge(cons(w + 1), RING, outfree, row0 + FROWS + 1, 1);
-        wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + FROWS, 2);
-        QPack<QT> q[T];
+        wait_ge(&cnt[CI_PRODQ], 0, qavail, row0 + 2 * FROWS, 2);
+        QPack<QT> qn[T];
 #pragma unroll
-        for (int k = 0; k < T; k++) q[k].load(qcol[k] + ((unsigned)row0 & qmask));
+        for (int k = 0; k < T; k++) qn[k].load(qcol[k] + ((unsigned)(row0 + FROWS) & qmask));
         // row m inside this chunk (uniform; -1: none / not the stripe holding column n)
         const int um = __builtin_amdgcn_readfirstlane((has_n && m - 1 - row0 < FROWS) ? m - 1 - row0 : -1);
         uint32_t acc[T][4 * CB];
@@ -698,6 +820,8 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
                     tbw[d * 64 + k] = make_uint4(acc[k][4 * d], acc[k][4 * d + 1], acc[k][4 * d + 2], acc[k][4 * d + 3]);
             tbw += CB * 64;
         }
+#pragma unroll
+        for (int k = 0; k < T; k++) q[k] = qn[k];
     }
     if (lane == 63) rout[mpad & RMASK].x = Hprev[T - 1];
     if (lane == 0) __hip_atomic_store(prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
@@ -1537,21 +1661,36 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
 
 // ----------------------------------------------------------------------------------
 // host-side launchers (called from ga_host.cpp)
+int boundary_scratch_ints(int m, int n) { return (m + BSEG - 1) / BSEG + (n + BSEG - 1) / BSEG + 2; }
+
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,
                      int o, int big, int* GVp, int* GHp, int2* top, int2* left, int* bnd_row, int* bnd_col, int* meta,
-                     bool custom) {
-    if (custom)
+                     bool custom, int* scratch) {
+    if (custom) {
         custom_boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, GVp, GHp, top, left, bnd_row, bnd_col, meta);
-    else
+        return;
+    }
+    if ((long long)m + n < 64 * 1024) {  // small problems: one workgroup does it all
         boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, big, GVp, GHp, top, left, bnd_row, bnd_col, meta);
+        return;
+    }
+    const int nba = (m + BSEG - 1) / BSEG, nbb = (n + BSEG - 1) / BSEG;
+    bnd_sums_kernel<<<nba + nbb, 256, 0, s>>>(a, m, b, n, gh, gv, nba, scratch);
+    bnd_scan_kernel<<<1, 1024, 0, s>>>(scratch, nba, nbb);
+    bnd_apply_kernel<<<nba + nbb, 256, 0, s>>>(a, m, b, n, gh, gv, nba, scratch, GVp, GHp);
+    bnd_edges_kernel<<<(std::max(m, n) + 256) / 256, 256, 0, s>>>(m, n, o, big, GVp, GHp, top, left, bnd_row, bnd_col,
+                                                                  meta);
 }
 
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows) {
     return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * qrows * qbytes;
 }
 
-template <int CB, typename QT, bool TB, bool FULL, int NWC, int T>
+template <int CB, typename QT, bool TB, bool FULL, int NWC, int T, bool DBG = false>
 static void launch_one(hipStream_t s, const FillArgs& p) {
+    // timestamped variants for the diagnostics tools (1-byte words, int8 profiles only)
+    if constexpr (!DBG && CB == 1 && std::is_same<QT, int8_t>::value && !FULL)
+        if (p.dbg != nullptr) return launch_one<CB, QT, TB, FULL, NWC, T, true>(s, p);
     // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
     static const long floor_env = [] {
         const char* e = getenv("GA_FILL_LDS_FLOOR");
@@ -1559,7 +1698,7 @@ static void launch_one(hipStream_t s, const FillArgs& p) {
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
-    auto* fn = fill_kernel<CB, QT, TB, FULL, NWC, T>;
+    auto* fn = fill_kernel<CB, QT, TB, FULL, NWC, T, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
