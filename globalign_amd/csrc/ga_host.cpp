@@ -134,6 +134,30 @@ struct Quad {
     }
 };
 
+// Branch-free form of the same table: next draw index, whether a dispatch completes inside the
+// quartet and the word offset (+1) of its 18th acceptance.
+struct QuadEntry2 {
+    uint32_t bytes;
+    uint8_t nacc, nd, wrap, woff;
+};
+struct Quad2 {
+    QuadEntry2 e[18][256];
+    Quad2() {
+        static const Quad Q;
+        for (int d = 0; d < 18; d++)
+            for (int B = 0; B < 256; B++) {
+                const QuadEntry& q = Q.e[d][B];
+                const unsigned nacc = q.meta & 7u;
+                QuadEntry2& r = e[d][B];
+                r.bytes = q.bytes;
+                r.nacc = (uint8_t)nacc;
+                r.nd = (uint8_t)((d + nacc) % 18);
+                r.wrap = (uint8_t)(d + nacc >= 18);
+                r.woff = r.wrap ? (uint8_t)(((q.meta >> (3 + 2 * (17 - d))) & 3u) + 1) : 0;
+            }
+    }
+};
+
 struct RngTable {
     std::vector<uint32_t> tab;        // per dispatch: level per candidate set (see dispatch_entry)
     std::vector<uint32_t> step_end;   // words consumed after each dispatch
@@ -154,8 +178,25 @@ inline void temper_block(const uint32_t* mt, uint32_t* out) {
     }
 }
 
+// The per-step entries from the accepted draws (18 per dispatch; draws 0-3 / 9-12 decide).
+void fill_entries(const uint8_t* acc, int64_t steps, RngTable& R) {
+    for (int64_t st = 0; st < steps; st++) {
+        const uint8_t* r = acc + 18 * st;
+        uint32_t e = 0;
+        for (int half = 0; half < 2; half++) {
+            const uint8_t* qq = r + 9 * half;
+            const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
+            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 16 * half);
+        }
+        R.tab[st] = e;
+    }
+}
+
+// The table of `steps` dispatches from the 625-word state (MT array + index).  Twisting and
+// tempering the stream is the cost (~9 ms for 2*10^5 dispatches on an EPYC 9575F); it runs
+// while the device fills.  (A producer/consumer split over two threads measured no faster.)
 void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
-    static const Quad Q;
+    static const Quad2 Q;
     PyMT g;
     std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
     g.mti = (int)state[MTN];
@@ -163,11 +204,12 @@ void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
     R.twist_snap.clear();
     R.twist_snap.push_back(g);
     R.tab.assign(steps, 0);
-    R.step_end.assign(steps, 0);
     const int64_t need = 18 * steps;
     std::vector<uint8_t> acc(need + 8);
+    std::vector<uint32_t> ends(steps + 4);
+    int64_t stp = 0;
     uint32_t words[MTN + 4];
-    int64_t p = 0, wbase = 0, k = 0, ntw = 0;
+    int64_t p = 0, wbase = 0, ntw = 0;
     unsigned d = 0;
     // the partial first block: words mti0 .. 623 of the initial array
     int first = g.mti, count = MTN - g.mti;
@@ -187,17 +229,12 @@ void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
         for (; q + 4 <= count && p < need; q += 4) {
             const unsigned B = (words[q] >> 30) | ((words[q + 1] >> 30) << 2) | ((words[q + 2] >> 30) << 4) |
                                ((words[q + 3] >> 30) << 6);
-            const QuadEntry& e = Q.e[d][B];
-            const unsigned nacc = e.meta & 7u;
+            const QuadEntry2& e = Q.e[d][B];
             std::memcpy(acc.data() + p, &e.bytes, 4);
-            if (d + nacc >= 18) {  // the step completes inside this quartet
-                const unsigned t = 17 - d;
-                const int64_t st = (p + t) / 18;
-                if (st < steps) R.step_end[st] = (uint32_t)(wbase + q + ((e.meta >> (3 + 2 * t)) & 3u) + 1);
-            }
-            p += nacc;
-            d += nacc;
-            if (d >= 18) d -= 18;
+            ends[stp] = (uint32_t)(wbase + q + e.woff);  // branch-free: kept only when a dispatch completes
+            stp += e.wrap;
+            p += e.nacc;
+            d = e.nd;
         }
         // tail words of the block (count not a multiple of 4), one at a time
         static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
@@ -205,7 +242,7 @@ void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
             const unsigned r = words[q] >> 30;
             if (r < sz[d]) {
                 acc[p] = (uint8_t)r;
-                if (d == 17) R.step_end[p / 18] = (uint32_t)(wbase + q + 1);
+                if (d == 17) ends[stp++] = (uint32_t)(wbase + q + 1);
                 p++;
                 d = d == 17 ? 0 : d + 1;
             }
@@ -213,17 +250,9 @@ void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
         wbase += count;
         count = 0;
     }
-    (void)k;
-    for (int64_t st = 0; st < steps; st++) {
-        const uint8_t* r = acc.data() + 18 * st;
-        uint32_t e = 0;
-        for (int half = 0; half < 2; half++) {
-            const uint8_t* qq = r + 9 * half;
-            const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
-            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 16 * half);
-        }
-        R.tab[st] = e;
-    }
+    ends.resize(steps);
+    R.step_end = std::move(ends);
+    fill_entries(acc.data(), steps, R);
 }
 
 // MT state after the first D dispatches consumed their words.

@@ -36,7 +36,7 @@ def _choice_levels(r):
     return out
 
 
-@pytest.mark.parametrize("seed,steps", [(0, 1), (1, 37), (12345, 500), (7, 3000)])
+@pytest.mark.parametrize("seed,steps", [(0, 1), (1, 37), (12345, 500), (7, 3000), (3, 5000), (11, 20000), (14, 4096)])
 def test_tiebreak_table_matches_cpython(lib, seed, steps):
     lib.ga_debug_rng.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
     random.seed(seed)
