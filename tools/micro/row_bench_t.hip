@@ -57,7 +57,8 @@ int main() {
     struct K { const char* name; void (*f)(long long*, int*, int); int T; };
     std::vector<K> ks = {{"T=1 score", rows<1, false>, 1}, {"T=2 score", rows<2, false>, 2},
                          {"T=4 score", rows<4, false>, 4}, {"T=1 tb", rows<1, true>, 1},
-                         {"T=2 tb", rows<2, true>, 2},     {"T=4 tb", rows<4, true>, 4}};
+                         {"T=2 tb", rows<2, true>, 2},     {"T=4 tb", rows<4, true>, 4},
+                         {"T=8 score", rows<8, false>, 8}};
     for (auto& k : ks) {
         printf("%-10s", k.name);
         for (int w = 1; w <= 4; w++) {
