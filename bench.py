@@ -13,6 +13,8 @@ Workloads (BASELINE.json configs, SURVEY 8d SplitMix64 inputs, resident in HBM):
                 find_global_alignment DP (fill + tie-break table + walk + strings,
                 globaligner.py:258-302).  At N=1 the default run also measures this headline
                 config and reports it as "headline_c3".
+  c4tb:         C4 with full traceback on one GPU: 10^12 traceback bytes do not fit in HBM, so the
+                traceback runs in row bands (a checkpointing score pass, then band refills + walk).
   c5:           20k x 20k protein (seeds 3, 4), BLOSUM62, gap_open_score -10, full traceback.
   c2:           10k x 10k DNA, full traceback.
 """
@@ -43,6 +45,9 @@ WORKLOADS = {
                     "full traceback"),
     "c4": dict(m=1_000_000, n=1_000_000, traceback=False, alphabet="dna", seeds=(1, 2), scoring=SCORING,
                desc="C4: 1M x 1M DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / ext -1, score only"),
+    "c4tb": dict(m=1_000_000, n=1_000_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING, golden="c4",
+                 desc="C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / "
+                      "ext -1; banded traceback (checkpointed score pass + band refills, DESIGN.md 5.5)"),
     "c5": dict(m=20_000, n=20_000, traceback=True, alphabet="protein", seeds=(3, 4), scoring=PROTEIN_SCORING,
                desc="C5: 20k x 20k protein (SplitMix64 seeds 3,4), BLOSUM62, gap_open_score -10, full traceback"),
 }
@@ -212,7 +217,7 @@ def main():
         from globalign_amd import distributed
         return distributed.bench_main(args, wl, args.workload)
     r = measure_single(wl, args.steps, args.warmup)
-    gold = golden_cost(args.workload)
+    gold = golden_cost(wl.get("golden", args.workload))
     line = {
         "metric": METRIC,
         "value": r["value"],

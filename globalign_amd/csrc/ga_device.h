@@ -34,7 +34,9 @@ struct FillArgs {
     int nwc, qrows;                     // compute waves per workgroup; LDS query-profile ring rows
     int cols_per_lane;                  // T: columns per lane (a stripe is 64*T columns; 1, 2 or 4)
     unsigned spin_limit, halo_spin_limit;
-    unsigned long long* dbg;  // optional timestamps: [nstripes][4] (s_memrealtime) or nullptr
+    unsigned long long* dbg;  // optional timestamps: [nstripes][8] or nullptr
+    int2* ckpt;               // banded traceback: (H', h2') of rows ckpt_rows, 2*ckpt_rows, ... (< m) or nullptr
+    int ckpt_rows;            //   [row / ckpt_rows - 1][n + 1]; a multiple of FROWS
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),
@@ -53,6 +55,7 @@ struct WalkArgs {
     int m, n, o;          // n: this slab's columns
     int i0, j0, L0, first0, D0, h0;  // start state (j0 local); a whole problem starts at (m, n, 0, 1, 0, 0)
     int handoff;          // 1: the slab has columns to its left; reaching local column 0 ends the walk here
+    int vhandoff;         // 1: a traceback band with rows above it; reaching local row 0 ends it (reason 6)
     int maxh;             // the reference's move bound m + n (global n)
     uint32_t* ops;        // out: 2-bit levels, dispatch D at bits 30 - 2*(D & 15) of word D >> 4
     int* result;          // out: [D, i, j, reason, diagnostics...]
@@ -64,7 +67,7 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
                      bool custom, int* scratch);
 int boundary_scratch_ints(int m, int n);  // ints of scratch launch_boundary needs
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
-size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows);
+size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows, int tb_stage_bytes_per_wave = 0);
 void launch_walk(hipStream_t s, const WalkArgs& w);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)
 void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full);

@@ -299,6 +299,7 @@ struct ga_ctx {
     std::vector<uint8_t> h_a, h_b;
     // device buffers
     DevBuf a, b, sub, gh, gv, qp, GVp, GHp, top, left, bnd_row, bnd_col, meta, hand, flags, tb, out_last, full, rng, bscr,
+        ckpt,
         ops, result;
     DevBuf halo_in{nullptr, 0, true};
     bool slab = false;
@@ -331,8 +332,9 @@ int check_ctx(ga_ctx* c) {
 // workgroup chains 4 waves (one per SIMD) when every stripe gets a wave that way, else 8.
 void set_stripes(ga_ctx* c, int T_req, bool tb, bool full) {
     const int64_t simds = 4 * (int64_t)c->num_cu;
-    // the FULL debug output is T == 1 only; T == 8 is score only (register budget)
-    const int cap = full ? 1 : tb ? 4 : 8;
+    // register budget (no spills, see the code objects' vgpr_spill_count): the FULL debug output is
+    // T == 1 only; traceback words T <= 2; score only T <= 8 with an int8 profile, 4 with int16
+    const int cap = full ? 1 : tb ? 2 : (c->qbytes == 2 ? 4 : 8);
     int T = 1;
     if (T_req == 1 || T_req == 2 || T_req == 4 || T_req == 8) {
         T = std::min(T_req, cap);
@@ -432,7 +434,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
         // query-profile ring: as many rows as fit 64 KB (at least 128)
         c->qrows = 1024;
         while (c->qrows > 128 && (size_t)K * c->qrows * c->qbytes > 64 * 1024) c->qrows >>= 1;
-        if (std::max(ga::fill_lds_bytes(8, c->qbytes, K, c->qrows), ga::fill_diag_lds_bytes(8, c->qbytes, K, c->qrows)) >
+        if (std::max(ga::fill_lds_bytes(8, c->qbytes, K, c->qrows, 8192), ga::fill_diag_lds_bytes(8, c->qbytes, K, c->qrows)) >
             160 * 1024)
             return fail(GA_E_RANGE, "alphabet too large for the LDS query profile");
     }
@@ -452,17 +454,28 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     return GA_OK;
 }
 
+// A band of rows of the whole problem (banded traceback): rows r0+1 .. r0+mb, its
+// top row from a checkpoint (nullptr: row 0), no boundary pass; or the checkpointing pass itself.
+struct Band {
+    int64_t r0 = 0, mb = 0;
+    const int2* top = nullptr;  // (H', h2') of row r0, [n+1] (column 0 = the left edge's corner)
+    bool band = false;          // fill rows r0+1 .. r0+mb only (the boundary is already computed)
+    int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
+    int ckpt_rows = 0;
+};
+
 // Enqueue boundary + query profile + fill.  Does not synchronise.
-int enqueue_fill(ga_ctx* c, int32_t flags) {
+int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
     const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
     const bool full = (flags & GA_FILL_FULL) != 0;
-    const int64_t m = c->m, n = c->n;
+    const int64_t m = bd.band ? bd.mb : c->m, n = c->n;
     // 16-row chunks; CB 16-byte words per lane per chunk (ga_device.h)
     c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
     // score only: the anti-diagonal kernel (64-column stripes) when asked for and its profile
     // ring is deep enough for a workgroup's skew (8 waves x 64 steps)
-    c->diag = (!tb || (full && c->qbytes == 1 && c->nstripes <= 4 * c->num_cu)) && c->diag_req == 2 && c->qrows >= 1024;
+    c->diag = (!tb || (full && c->qbytes == 1 && c->nstripes <= 4 * c->num_cu)) && c->diag_req == 2 && c->qrows >= 1024 &&
+              bd.ckpt == nullptr;
     set_stripes(c, c->diag ? 1 : c->T_req, tb, full);
     if (c->diag && full) {  // the debug FULL variant is built for 4 compute waves
         c->nwc = 4;
@@ -479,21 +492,24 @@ int enqueue_fill(ga_ctx* c, int32_t flags) {
     unsigned* fl = c->flags.as<unsigned>();
     // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
-    ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global, c->gh.as<int>(),
-                        c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(), c->top.as<int2>(),
-                        c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(), c->meta.as<int>(), c->custom,
-                        c->bscr.as<int>());
+    if (!bd.band)
+        ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global,
+                            c->gh.as<int>(), c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(),
+                            c->top.as<int2>(), c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(),
+                            c->meta.as<int>(), c->custom, c->bscr.as<int>());
     ga::FillArgs p{};
-    p.a = c->a.as<uint8_t>();
+    p.a = c->a.as<uint8_t>() + bd.r0;
+    p.ckpt = bd.ckpt;
+    p.ckpt_rows = bd.ckpt_rows;
     p.subp = c->qp.as<int>();
     p.K = c->K;
     p.b = c->b.as<uint8_t>() + c->col0;
-    p.top = c->top.as<int2>() + c->col0;
+    p.top = (bd.top ? bd.top : c->top.as<int2>()) + c->col0;
     if (c->slab && c->col0 > 0) {
         p.left = c->halo_in_ext ? c->halo_in_ext : c->halo_in.as<int2>();
         p.left_prog = c->prog_dev;  // [0]: halo_in rows
     } else {
-        p.left = c->left.as<int2>();
+        p.left = c->left.as<int2>() + bd.r0;
         p.left_prog = nullptr;
     }
     p.hand = c->hand.as<int2>();
@@ -578,22 +594,24 @@ struct WalkStart {
     int L, first;
 };
 
-int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st) {
-    HIPCHK(hipMemcpyAsync(c->rng.p, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, c->stream));
+int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, int64_t r0 = 0, int64_t mb = -1,
+             bool vhandoff = false, bool upload_tab = true) {
+    if (upload_tab) HIPCHK(hipMemcpyAsync(c->rng.p, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, c->stream));
     ga::WalkArgs w{};
     w.tb = c->tb.as<uint8_t>();
     w.CB = c->CB;
     w.TC = c->TC;
-    w.a = c->a.as<uint8_t>();
+    w.a = c->a.as<uint8_t>() + r0;
     w.b = c->b.as<uint8_t>() + c->col0;
     w.bnd_row = c->bnd_row.as<int>() + 3 * c->col0;
-    w.bnd_col = c->bnd_col.as<int>();
+    w.bnd_col = c->bnd_col.as<int>() + 3 * r0;
     w.rng = c->rng.as<uint32_t>();
     w.nrng = (long long)ntab;
-    w.m = (int)c->m;
+    w.m = (int)(mb >= 0 ? mb : c->m);
     w.n = (int)c->n;
     w.o = c->o;
-    w.i0 = (int)st.i;
+    w.i0 = (int)(st.i - r0);
+    w.vhandoff = vhandoff ? 1 : 0;
     w.j0 = (int)(st.j - c->col0);
     w.L0 = st.L;
     w.first0 = st.first;
@@ -670,6 +688,11 @@ int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const
     return GA_OK;
 }
 
+// The end of a traceback: the MT state after its dispatches, the reference's tails, reversal.
+int conclude_walk(const RngTable& snaps, const WalkStart& st, int reason, uint32_t* mt_state, const char* a_chr,
+                  const char* b_chr, char* oa, char* om, char* ob, int64_t cap, int64_t len, int64_t* out_len,
+                  int32_t* tb_status);
+
 // Whole-problem traceback: one walk from (m, n), tails, reversal (dp_array_backward's output).
 int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char* a_chr, const char* b_chr,
                 char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
@@ -677,6 +700,12 @@ int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char
     int reason = 0;
     int64_t len = 0;
     if (int r = walk_segment(c, st, reason, a_chr, b_chr, oa, om, ob, cap, len)) return r;
+    return conclude_walk(snaps, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
+}
+
+int conclude_walk(const RngTable& snaps, const WalkStart& st, int reason, uint32_t* mt_state, const char* a_chr,
+                  const char* b_chr, char* oa, char* om, char* ob, int64_t cap, int64_t len, int64_t* out_len,
+                  int32_t* tb_status) {
     state_after(snaps, st.D, mt_state);
     if (reason == 4) {  // IndexError in the reference
         *tb_status = GA_TB_INDEX_ERROR;
@@ -698,6 +727,83 @@ int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char
     *out_len = len;
     *tb_status = GA_TB_OK;
     return GA_OK;
+}
+
+// ---------------------------------------------------------------- banded traceback
+// Traceback words take m*n*CB bytes.  Past a budget (GA_TB_BUDGET_MB, default 64 GB of the 288 GB),
+// the traceback runs in bands of Bh rows: one score-only fill that also saves the
+// (H', h2') row every Bh rows, then, from the bottom band up, a fill of the band's rows with
+// traceback words (its top row from the checkpoint) and the walk through it, handed on at the
+// band's top row (walk reason 6).  Fill work doubles; memory is one band of words.
+int64_t band_rows(ga_ctx* c) {
+    if (const char* e = getenv("GA_TB_BAND_ROWS")) {  // tests: force (small) bands
+        const int64_t Bh = (atoll(e) / ga::FROWS) * ga::FROWS;
+        return Bh >= ga::FROWS && c->m >= 2 * Bh ? Bh : 0;
+    }
+    int64_t budget = (int64_t)64 << 30;
+    if (const char* e = getenv("GA_TB_BUDGET_MB")) budget = atoll(e) << 20;
+    const int64_t words = ((c->n + 63) / 64) * 64 * c->CB;  // traceback bytes per row
+    if (c->m * words <= budget) return 0;
+    const int64_t Bh = std::max<int64_t>(64, (budget / words / ga::FROWS) * ga::FROWS);
+    return c->m >= 2 * Bh ? Bh : 0;
+}
+
+int check_fill_abort(ga_ctx* c) {
+    unsigned abort_word = 0;
+    HIPCHK(hipMemcpy(&abort_word, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (abort_word) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+    return GA_OK;
+}
+
+int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
+                 char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const double t0 = now_ms();
+    const int64_t m = c->m, n = c->n;
+    // bands [b*Bh, b*Bh + Bh) of rows, the last one absorbing a remainder of < 16 rows
+    int64_t nb = (m + Bh - 1) / Bh;
+    if (nb > 1 && m - (nb - 1) * Bh < ga::FROWS) nb--;
+    const int64_t nck = (m - 1) / Bh;  // checkpoint rows the fill writes (every multiple of Bh below m)
+    HIPCHK(c->ckpt.ensure(sizeof(int2) * (size_t)std::max<int64_t>(nck, 1) * (n + 1)));
+    int2* ck = c->ckpt.as<int2>();
+    Band pass1;
+    pass1.ckpt = ck;
+    pass1.ckpt_rows = (int)Bh;
+    if (int r = enqueue_fill(c, 0, pass1)) return r;
+    RngTable R;
+    const double t1 = now_ms();
+    build_rng(mt_state, m + n + 1, R);
+    c->rng_ms = (float)(now_ms() - t1);
+    if (int r = finish_fill(c, cost_out, nullptr)) return r;
+    WalkStart st{m, n, 0, 0, 0, 1};
+    int reason = 6;
+    int64_t len = 0;
+    float walk_ms = 0.f, fill_ms = c->fill_ms;
+    for (int64_t b = nb - 1; b >= 0 && reason == 6; b--) {
+        Band bd;
+        bd.band = true;
+        bd.r0 = b * Bh;
+        bd.mb = b == nb - 1 ? m - bd.r0 : Bh;
+        if (b > 0) {
+            int2* row = ck + (size_t)(b - 1) * (n + 1);
+            // column 0 of the checkpoint row: the left edge's corner H'(r0, 0)
+            HIPCHK(hipMemcpyAsync(row, c->left.as<int2>() + bd.r0, sizeof(int2), hipMemcpyDeviceToDevice, c->stream));
+            bd.top = row;
+        }
+        if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
+        if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), st, bd.r0, bd.mb, b > 0, b == nb - 1)) return r;
+        int64_t seg = 0;
+        if (int r = walk_segment(c, st, reason, a_chr, b_chr, oa + len, om + len, ob + len, cap - len, seg)) return r;
+        if (int r = check_fill_abort(c)) return r;
+        len += seg;
+        walk_ms += c->walk_ms;
+        float f = 0.f;
+        if (hipEventElapsedTime(&f, c->ev[0], c->ev[1]) == hipSuccess) fill_ms += f;
+    }
+    c->walk_ms = walk_ms;
+    c->fill_ms = fill_ms;
+    const int rc = conclude_walk(R, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
+    c->call_ms = (float)(now_ms() - t0);
+    return rc;
 }
 
 }  // namespace
@@ -752,7 +858,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
-                      &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr})
+                      &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& e : c->ev)
@@ -792,6 +898,8 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     if (int r = check_ctx(c)) return r;
     if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
+    if (const int64_t Bh = band_rows(c)) return banded_align(c, Bh, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len,
+                                                             tb_status, cost_out);
     const double t0 = now_ms();
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK)) return r;
     // the tie-break table is built on the host while the device fills

@@ -363,7 +363,14 @@ enum { CI_PC = 0, CI_PROD0 = 31, CI_ABORT = 32, CI_SLAB = 33, CI_PRODQ = 34 };
 constexpr int FILL_CNT_BYTES = 256;
 
 template <int CB, typename QT, bool TB, int T, bool DBG>
-__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane);
+__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, uint4* tbstage, int w, int g, int lane);
+
+// LDS staging of a blocked wave's traceback words (T > 1): 16-byte words per lane per chunk
+template <int CB, int T>
+struct TbStage {
+    static constexpr int UINT4S = T > 1 ? T * CB * 64 : 0;  // per compute wave
+};
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // DBG: per-stripe timestamps into p.dbg (s_memtime shares lgkmcnt with LDS reads, so the
 // timing code stays out of the production variants)
@@ -407,7 +414,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         int2* rin0 = ring;
         const int2* rout = ring + nlive * RING;
         const int K = p.K;
-        const int h00 = p.top[g * NWC * 64].x;  // H'(0, left edge)
+        const int h00 = p.top[g * NWC * 64 * T].x;  // H'(0, left edge of this workgroup's columns)
         unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
         while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
@@ -488,7 +495,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     }
     if (w >= nlive) return;
     if constexpr (T > 1) {
-        fill_blocked<CB, QT, TB, T, DBG>(p, cnt, ring, qring, w, g, lane);
+        uint4* tbstage = reinterpret_cast<uint4*>(
+                             smem + align16((size_t)FILL_CNT_BYTES + (size_t)(NWC + 1) * RING * sizeof(int2) +
+                                            (size_t)p.K * p.qrows * sizeof(QT))) +
+                         (size_t)w * TbStage<CB, T>::UINT4S;
+        fill_blocked<CB, QT, TB, T, DBG>(p, cnt, ring, qring, tbstage, w, g, lane);
         return;
     }
 
@@ -651,6 +662,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         }
 #pragma unroll
         for (int k = 0; k < 4 * CB; k++) accP[k] = acc[k];
+        // checkpoint row (banded traceback): (H', h2') of every column after row row0+16
+        if (p.ckpt != nullptr && (row0 + FROWS) % p.ckpt_rows == 0 && row0 + FROWS < m && colok)
+            p.ckpt[(long long)((row0 + FROWS) / p.ckpt_rows - 1) * (p.n + 1) + jcol] = make_int2(Hprev, Yc);
     }
     if (TB) {
         // the last sub-chunk's codes, then the last chunk's words
@@ -687,7 +701,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
 // 64-column layout of ga_device.h: column (l, k) is lane (l*T + k) % 64 of 64-column stripe
 // T*s + (l*T) / 64, so a lane's T words are one contiguous 16*T-byte run.
 template <int CB, typename QT, bool TB, int T, bool DBG>
-__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, int w, int g, int lane) {
+__device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, uint4* tbstage, int w, int g, int lane) {
     __builtin_amdgcn_s_setprio(2);
     unsigned* abort_sh = cnt + CI_ABORT;
     auto prod = [&](int k) -> unsigned* { return k == 0 ? cnt + CI_PROD0 : cnt + 2 * k - 1; };
@@ -720,8 +734,8 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
     const unsigned op1 = (unsigned)o + 1u;
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
-    uint4* tbw = TB ? reinterpret_cast<uint4*>(p.tb) + ((long long)(T * s + (lane * T) / 64) * p.TC) * 64 + (lane * T) % 64
-                    : nullptr;
+    // traceback words: this wave's T 64-column stripes T*s .. T*s+T-1; lane = column within a stripe
+    uint4* tbg = TB ? reinterpret_cast<uint4*>(p.tb) + ((long long)(T * s) * p.TC) * 64 + lane : nullptr;
     unsigned avail = 0, outfree = 0, qavail = 0;
     const unsigned pc_lds = lds_addr(cons(w));  // {cons[w], prod[w + 1]}
     const unsigned rout_lds = lds_addr(rout);
@@ -813,15 +827,32 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
             e23 = n23;
         }
         if (TB) {
+            // through LDS so that every global store is one whole 1 KiB run of a 64-column stripe
+            // (a lane's own T words sit 16*T bytes apart in it: stored directly, each store
+            // instruction would write a 1/T-dense pattern and HBM sees ~9x the bytes at T = 4)
+            const int sl = (lane * T) >> 6, l0 = (lane * T) & 63;
 #pragma unroll
             for (int d = 0; d < CB; d++)
 #pragma unroll
                 for (int k = 0; k < T; k++)
-                    tbw[d * 64 + k] = make_uint4(acc[k][4 * d], acc[k][4 * d + 1], acc[k][4 * d + 2], acc[k][4 * d + 3]);
-            tbw += CB * 64;
+                    tbstage[(sl * CB + d) * 64 + l0 + k] =
+                        make_uint4(acc[k][4 * d], acc[k][4 * d + 1], acc[k][4 * d + 2], acc[k][4 * d + 3]);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // one wave's LDS operations execute in order
+#pragma unroll
+            for (int s2 = 0; s2 < T; s2++)
+#pragma unroll
+                for (int d = 0; d < CB; d++) tbg[(size_t)s2 * p.TC * 64 + d * 64] = tbstage[(s2 * CB + d) * 64 + lane];
+            tbg += CB * 64;
         }
 #pragma unroll
         for (int k = 0; k < T; k++) q[k] = qn[k];
+        // checkpoint row (banded traceback): (H', h2') of every column after row row0+16
+        if (p.ckpt != nullptr && (row0 + FROWS) % p.ckpt_rows == 0 && row0 + FROWS < m) {
+            int2* ck = p.ckpt + (long long)((row0 + FROWS) / p.ckpt_rows - 1) * (n + 1);
+#pragma unroll
+            for (int k = 0; k < T; k++)
+                if (jl + k + 1 <= n) ck[jl + k + 1] = make_int2(Hprev[k], Yc[k]);
+        }
     }
     if (lane == 63) rout[mpad & RMASK].x = Hprev[T - 1];
     if (lane == 0) __hip_atomic_store(prod(w + 1), (unsigned)(mpad + 1), RLX, WGS);
@@ -1435,6 +1466,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     __builtin_amdgcn_s_setprio(3);
     int i = w.i0, j = w.j0, L = w.L0, D = w.D0, h = w.h0, first = w.first0, reason = -1;
     const int jend = w.handoff ? 5 : 2;  // reason when the walk reaches local column 0
+    const int iend = w.vhandoff ? 6 : 1;  // ... and local row 0 (a traceback band with rows above it)
     int cti = -1, ctj = -1, nwait = 0, ntiles = 0, ndbg = 0;
     const int maxh = w.maxh;
     unsigned long long t_tile = 0, t_ring = 0;  // time spent waiting (s_memrealtime ticks, 100 MHz)
@@ -1525,10 +1557,10 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
         L = lvl;
         if (first) {
             first = 0;
-            if (i == 0 && j == 0) { reason = 0; break; }
+            if (i == 0 && j == 0 && !w.vhandoff) { reason = 0; break; }
             continue;
         }
-        if (i == 0) { reason = 1; break; }
+        if (i == 0) { reason = iend; break; }
         if (j == 0) { reason = jend; break; }
         if (++h >= maxh) { reason = 3; break; }
     }
@@ -1639,7 +1671,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                 const int nd = 4 * g + k;
                 opsbuf[(D >> 4) & (RB / 16 - 1)] = ops << (2 * (16 - nd));
                 D += nd;
-                reason = i == 0 ? 1 : jend;
+                reason = i == 0 ? iend : jend;
                 break;
             }
             opsbuf[(D >> 4) & (RB / 16 - 1)] = ops;
@@ -1682,8 +1714,9 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
                                                                   meta);
 }
 
-size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows) {
-    return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * qrows * qbytes;
+size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows, int tb_stage_bytes_per_wave) {
+    return align16((size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * qrows * qbytes) +
+           (size_t)nwc * tb_stage_bytes_per_wave;
 }
 
 template <int CB, typename QT, bool TB, bool FULL, int NWC, int T, bool DBG = false>
@@ -1697,7 +1730,8 @@ static void launch_one(hipStream_t s, const FillArgs& p) {
         return e ? atol(e) : -1L;
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
-    const size_t lds = std::max<size_t>(fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
+    const size_t lds = std::max<size_t>(
+        fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows, TB ? TbStage<CB, T>::UINT4S * 16 : 0), floor_b);
     auto* fn = fill_kernel<CB, QT, TB, FULL, NWC, T, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
@@ -1705,8 +1739,9 @@ static void launch_one(hipStream_t s, const FillArgs& p) {
 
 template <typename QT, int NWC, int T>
 static void launch_fill_t(hipStream_t s, const FillArgs& p, int CB, bool tb, bool full) {
-    if (!tb) return launch_one<1, QT, false, false, NWC, T>(s, p);
-    if constexpr (T == 8) return;  // score only (the host never asks for it with traceback words)
+    if constexpr (T == 8 && sizeof(QT) == 2) return;  // register budget: the host never asks for these
+    else if (!tb) return launch_one<1, QT, false, false, NWC, T>(s, p);
+    if constexpr (T > 2) return;  // traceback words: T <= 2 (register budget)
     else {
     if constexpr (T == 1) {
         if (full) {
