@@ -91,3 +91,26 @@ def test_blocked_multi_round_score_vs_oracle(monkeypatch, T):
     big = (tab.max_cost + 1) * max(len(s1), len(s2))
     row0, col0 = core.boundary(tab, a, b, goc, big)
     assert int(cost) == int(min(core.fill_score_parallel(tab, a, b, goc, row0, col0, 8)))
+
+
+@pytest.mark.parametrize("T", [1, 2, 4, 8])
+def test_blocked_custom_boundary_vs_oracle(monkeypatch, T):
+    """Host-supplied row-0 / column-0 triples (dp_array_forward on a caller's dp_array, globaligner.py:366-392):
+    every workgroup's first row takes its corner from the top row, at every stripe width."""
+    from oracle import core
+    rng = np.random.default_rng(T)
+    m, n = 700, 5000
+    s1, s2 = splitmix_seq(m, 61, "dna"), splitmix_seq(n, 62, "dna")
+    tables, cmat, goc = _tables(s1, s2)
+    row0 = rng.integers(0, 60, size=3 * (n + 1)).astype(np.int64)
+    col0 = rng.integers(0, 60, size=3 * (m + 1)).astype(np.int64)
+    row0[:3] = col0[:3] = 0
+    tab = core.Tables(cmat)
+    want = int(min(core.fill_score(tab, tab.codes(s1), tab.codes(s2), goc, row0, col0)))
+    eng = _engine(monkeypatch, T)
+    try:
+        eng.load(tables.codes(s1), tables.codes(s2), tables, row0=row0, col0=col0)
+        got = int(eng.fill(traceback=False)[0])
+    finally:
+        eng.close()
+    assert got == want
