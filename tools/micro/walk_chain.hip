@@ -1,0 +1,54 @@
+// Microbenchmark: latency of the traceback walker's per-step dependent chain on gfx950 (one wave):
+// v_readlane of a window cell -> scalar ops -> the next readlane's lane index.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+template <int V>
+__global__ void chain(long long* out, int* sink, int n) {
+    const int lane = threadIdx.x & 63;
+    int win = (lane * 37 + 11) & 0x7fff;
+    unsigned t = 0x9e3779b9u, idx = 0, L8 = 0, acc = 0;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < n; k++) {
+        if (V == 0) {  // the walker's step: readlane, field of the entering level, tie-break bits, move
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)(idx & 63));
+            const unsigned lvl = (t >> ((v >> L8) & 31u)) & 3u;
+            L8 = lvl << 3;
+            idx += (0x080109u >> L8) & 0xffu;
+            acc += lvl;
+        } else if (V == 1) {  // readlane -> one scalar add -> readlane
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)(idx & 63));
+            idx += v;
+        } else if (V == 2) {  // eight dependent scalar ops (no readlane)
+            idx = ((idx >> 3) ^ t) + 1u;
+            idx = (idx >> (idx & 7u)) & 0xffffu;
+            idx = idx * 5u + 3u;
+            idx = (idx >> 1) + (idx & 1u);
+        }
+    }
+    long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x] = t1 - t0;
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = (int)(idx + acc);
+}
+
+template <typename F>
+double run(F f) {
+    long long* d; int* s;
+    (void)hipMalloc(&d, 256 * 8);
+    (void)hipMalloc(&s, 256 * 64 * 4);
+    const int n = 1 << 16;
+    f<<<1, 64>>>(d, s, n);
+    f<<<1, 64>>>(d, s, n);
+    (void)hipDeviceSynchronize();
+    long long h = 0;
+    (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d); (void)hipFree(s);
+    return (double)h / n;
+}
+
+int main() {
+    printf("walker step (readlane + 8 SALU): %.1f cyc\n", run(chain<0>));
+    printf("readlane -> s_add -> readlane : %.1f cyc\n", run(chain<1>));
+    printf("8 dependent SALU ops          : %.1f cyc\n", run(chain<2>));
+    return 0;
+}
