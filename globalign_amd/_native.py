@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libglobalign_amd.so")
+LIB_PATH = os.environ.get("GA_LIB_PATH") or os.path.join(_HERE, "_lib", "libglobalign_amd.so")
 
 GA_FILL_TRACEBACK = 1
 GA_FILL_FULL = 2

@@ -10,7 +10,10 @@ namespace ga {
 constexpr int RING = 256;        // rows per LDS edge ring between consecutive waves
 constexpr int RMASK = RING - 1;
 constexpr int FROWS = 16;        // rows per fill chunk (one 16-byte traceback store per lane per CB)
-constexpr int GOUT = 16;         // rows per cross-workgroup publish
+#ifndef GA_GOUT
+#define GA_GOUT 16
+#endif
+constexpr int GOUT = GA_GOUT;    // rows per cross-workgroup publish
 constexpr int FILL_LDS_MIN = 82 * 1024;  // > 80 KB: one fill workgroup per CU
 
 struct FillArgs {

@@ -294,6 +294,7 @@ struct ga_ctx {
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
     int T = 1, T_req = 0, nwc_req = 0;
     int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal (GA_FILL_MODE)
+    int diag_T_req = 0;        // columns per lane of the anti-diagonal kernel (GA_DIAG_COLS_PER_LANE; 0: automatic)
     bool diag = false;         // the last enqueued fill used the anti-diagonal kernel      // columns per lane of the fill (T_req 0: automatic; GA_COLS_PER_LANE)
     int64_t GV_m = 0, GH_n = 0;
     std::vector<uint8_t> h_a, h_b;
@@ -474,12 +475,23 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
     // score only: the anti-diagonal kernel (64-column stripes) when asked for and its profile
     // ring is deep enough for a workgroup's skew (8 waves x 64 steps)
-    c->diag = (!tb || (full && c->qbytes == 1 && c->nstripes <= 4 * c->num_cu)) && c->diag_req == 2 && c->qrows >= 1024 &&
-              bd.ckpt == nullptr;
-    set_stripes(c, c->diag ? 1 : c->T_req, tb, full);
-    if (c->diag && full) {  // the debug FULL variant is built for 4 compute waves
-        c->nwc = 4;
-        c->nslabs = (c->nstripes + 3) / 4;
+    // (its query-profile ring deeper than a workgroup's skew: NWC stripes x 64*TD steps)
+    int qrows = c->qrows;
+    c->diag = false;
+    if ((!tb || (full && c->qbytes == 1)) && c->diag_req == 2 && bd.ckpt == nullptr) {
+        const int td = full ? std::min(std::max(c->diag_T_req, 1), 2) : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req : 2;
+        set_stripes(c, td, false, false);
+        if (full) {  // the debug FULL variant is built for 4 compute waves
+            c->nwc = 4;
+            c->nslabs = (c->nstripes + 3) / 4;
+        }
+        qrows = 8192;
+        while (qrows > 128 && (size_t)c->K * (qrows + 16) * c->qbytes > 64 * 1024) qrows >>= 1;
+        c->diag = qrows >= c->nwc * (64 * c->T + 16) + 64 * c->T + 64;
+    }
+    if (!c->diag) {
+        qrows = c->qrows;
+        set_stripes(c, c->T_req, tb, full);
     }
     // traceback words cover T 64-column stripes per fill stripe
     if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
@@ -528,7 +540,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.nslabs = c->nslabs;
     p.TC = c->TC;
     p.nwc = c->nwc;
-    p.qrows = c->qrows;
+    p.qrows = qrows;
     p.cols_per_lane = c->T;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
@@ -837,6 +849,7 @@ int ga_ctx_create(int device, ga_ctx** out) {
         if (const char* e = getenv("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
         if (const char* e = getenv("GA_FILL_NWC")) c->nwc_req = atoi(e);
         if (const char* e = getenv("GA_FILL_MODE")) c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : 0;
+        if (const char* e = getenv("GA_DIAG_COLS_PER_LANE")) c->diag_T_req = atoi(e);
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;

@@ -37,6 +37,11 @@ namespace ga {
 #define RLX __ATOMIC_RELAXED
 #define AGENT __HIP_MEMORY_SCOPE_AGENT
 #define WGS __HIP_MEMORY_SCOPE_WORKGROUP
+// row of a 4-row sub-chunk after which the row-scan waves await and read the next sub-chunk's
+// edges (0..3; tools/sweep14.sh: 2 is 2 % faster than 0 at C3, 1 % at C4)
+#ifndef GA_EDGE_U
+#define GA_EDGE_U 2
+#endif
 
 __device__ __forceinline__ unsigned lds_ld(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, WGS); }
 __device__ __forceinline__ unsigned sgpr_u(unsigned x) { return (unsigned)__builtin_amdgcn_readfirstlane((int)x); }
@@ -629,9 +634,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                         f[0] = M; f[1] = X; f[2] = Yc;
                     }
                 }
-                if (u == 0) {
-                    // after one row (the previous sub-chunk's ring writes have landed): check the
-                    // next sub-chunk's rows and read their edges, three rows before their use
+                if (u == GA_EDGE_U) {
+                    // after GA_EDGE_U + 1 rows: check the next sub-chunk's rows and read their edges,
+                    // 3 - GA_EDGE_U rows before their use (later = the stripe trails its left
+                    // neighbour by fewer rows; row 2 measured best: one row covers the LDS latency)
                     if (r0 + 4 < mpad) {
                         avail = sgpr_u(max(avail, pnext));
                         wait_ge(&pc.prod(w), 0, avail, r0 + 8);
@@ -810,7 +816,7 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
 #pragma unroll
                     for (int k = 0; k < T; k++) Hm[k] = Hprev[k];
                 }
-                if (u == 0) {
+                if (u == GA_EDGE_U) {
                     if (r0 + 4 < mpad) {
                         avail = sgpr_u(max(avail, pnext));
                         wait_ge(prod(w), 0, avail, r0 + 8, 0);
@@ -894,7 +900,7 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
 // cost come out of the same ring as for a full stripe.
 constexpr int QMIRROR = 16;
 
-template <typename QT, int NWC, bool FULL, bool DBG>
+template <typename QT, int NWC, int TD, bool FULL, bool DBG>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -911,7 +917,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     __syncthreads();
     const int g = __builtin_amdgcn_readfirstlane((int)cnt[CI_SLAB]);
     const int m = p.m, o = p.o;
-    const int nsteps = m + 63;                       // lane 63 reaches row m at step m + 62
+    const int nsteps = m + 64 * TD - 1;              // lane 63's last column reaches row m at step m + 64TD - 2
     const int nch = (nsteps + FROWS - 1) / FROWS;
     const unsigned rows_end = (unsigned)(nch * FROWS + 16);  // every row a consumer may ask for
     const int nlive = min(NWC, p.nstripes - g * NWC);
@@ -1005,20 +1011,29 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     }
     if (w >= nlive) return;
 
-    // ---------------- compute wave w: stripe s ----------------
+    // ---------------- compute wave w: stripe s (64*TD columns) ----------------
     __builtin_amdgcn_s_setprio(2);
     const int s = g * NWC + w;
-    const int j0 = s * 64;
-    const int jcol = j0 + lane + 1;
-    const bool colok = jcol <= p.n;
-    const bool partial = j0 + 64 > p.n;  // uniform: the stripe holding column n, when it is not whole
-    const int bcode = colok ? p.b[jcol - 1] : 0;
-    const QT* qcol = qring + bcode * QS;
-    int Hout = p.top[colok ? jcol : p.n].x;       // H'(i-1, j) before row i: H'(0, j)
-    int Yc = p.top[colok ? jcol : p.n].y;         // h2'(0, j)
-    int Hd = p.top[colok ? jcol - 1 : p.n].x;     // H'(0, j-1): the diagonal of row 1
-    int Xout = 0;
-    const unsigned rout_lds = lds_addr(ring + (w + 1) * RING);
+    const int j0 = s * 64 * TD;
+    const int jl = j0 + lane * TD;                // this lane: columns jl+1 .. jl+TD
+    const bool partial = j0 + 64 * TD > p.n;      // uniform: the stripe holding column n, when it is not whole
+    const QT* qcol[TD];
+    bool colok[TD];
+    // per column: H' of the last two steps (by step parity), the h1' it passes right, h2'
+    int Hp[2][TD], Xo[TD], Yc[TD];
+#pragma unroll
+    for (int k = 0; k < TD; k++) {
+        const int jc = jl + k + 1;
+        colok[k] = jc <= p.n;
+        qcol[k] = qring + (colok[k] ? p.b[jc - 1] : 0) * QS;
+        const int2 t = p.top[colok[k] ? jc : p.n];
+        Hp[0][k] = Hp[1][k] = t.x;                // H'(0, j) until the column reaches row 1
+        Yc[k] = t.y;                              // h2'(0, j)
+        Xo[k] = 0;
+    }
+    int Hd0 = p.top[min(jl, p.n)].x;              // column 0's diagonal: H'(0, jl) for row 1
+    int2* rout = ring + (w + 1) * RING;
+    const unsigned rout_lds = lds_addr(rout);
     const unsigned pc_lds = lds_addr(cons(w));  // {cons[w], prod[w + 1]}
     const unsigned long long edgemask = 1ull << 63;
     unsigned avail = 0, outfree = 0, qavail = 0;
@@ -1042,45 +1057,57 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
     const int2* rin = ring + w * RING;
-    // slot (r - 1) & RMASK of a ring holds (H', h1') of row r.  Edges are read two sub-chunks
-    // (8 steps) ahead and the profile one chunk ahead: a step is ~30 cycles, an LDS read ~100+.
-    wait_ge(prod(w), 0, avail, 8, 0);
-    int4 e01 = reinterpret_cast<const int4*>(rin)[0];  // rows 1..4 (sub-chunk 0)
-    int4 e23 = reinterpret_cast<const int4*>(rin)[1];
-    int4 f01 = reinterpret_cast<const int4*>(rin)[2];  // rows 5..8 (sub-chunk 1)
-    int4 f23 = reinterpret_cast<const int4*>(rin)[3];
-    int cH = 0, cX = 0;  // lane 63's (H', h1') of the last step of the previous sub-chunk
-    // this lane's 16 profile values of chunk 0: rows 1-l .. 16-l (never wrap: mirror tail)
+    const unsigned* prod_in = prod(w);
+    // slot (r - 1) & RMASK of a ring holds (H', h1') of row r.  Edges are read one sub-chunk
+    // (4 steps) ahead into ping-pong registers, the producer's counter one sub-chunk ahead of its
+    // use, the profile one chunk ahead.
+    wait_ge(prod(w), 0, avail, 4, 0);
+    int4 A01 = reinterpret_cast<const int4*>(rin)[0];  // rows 1..4 (sub-chunk 0)
+    int4 A23 = reinterpret_cast<const int4*>(rin)[1];
+    int4 B01, B23;
+    unsigned pnext = *prod_in;
+    int cH = 0, cX = 0;  // lane 63's last column's (H', h1') of the last step of the previous sub-chunk
+    // column k of this lane works on row t - (lane*TD + k) + 1 at step t: its 16 profile values of
+    // chunk 0 are rows 1-c .. 16-c (never wrap: mirror tail)
     wait_ge(&cnt[CI_PRODQ], 0, qavail, FROWS, 2);
-    QPack<QT> sub;
-    sub.load_unaligned(qcol + (((unsigned)(-lane)) & qmask));
+    QPack<QT> sub[TD];
+#pragma unroll
+    for (int k = 0; k < TD; k++) sub[k].load_unaligned(qcol[k] + (((unsigned)(-(lane * TD + k))) & qmask));
 
-    auto step = [&](int eh, int ex, int sub, bool masked, int t) {
-        const int HL = __builtin_amdgcn_update_dpp(eh, Hout, 0x138, 0xf, 0xf, false);  // wave_shr:1, lane 0: edge
-        const int XL = __builtin_amdgcn_update_dpp(ex, Xout, 0x138, 0xf, 0xf, false);
-        const int M = Hd + sub;
-        Hd = HL;
-        if (!masked) {
-            const int H = min(min(M, XL), Yc);
-            const int Ho = H + o;
-            Xout = min(XL, Ho);
-            Yc = min(Yc, Ho);
-            Hout = H;
-        } else {
-            const int i = t - lane + 1;
-            if (!colok) {  // columns past n forward their left input
-                Hout = HL;
-                Xout = XL;
-            } else if (i >= 1) {
-                const int H = min(min(M, XL), Yc);
+    // one step: the columns right to left, so that column k reads column k-1's values of the
+    // previous step (h1') and of the one before (H', the diagonal) before they are replaced
+    auto step = [&](int eh, int ex, int u, int t, auto MASKED) {
+        constexpr bool MK = decltype(MASKED)::value;
+        const int pp = u & 1;  // t and u have the same parity (t0 is a multiple of 16)
+        const int HL = __builtin_amdgcn_update_dpp(eh, Hp[pp ^ 1][TD - 1], 0x138, 0xf, 0xf, false);  // lane 0: edge
+        const int XL0 = __builtin_amdgcn_update_dpp(ex, Xo[TD - 1], 0x138, 0xf, 0xf, false);
+#pragma unroll
+        for (int k = TD - 1; k >= 0; k--) {
+            const int M = (k == 0 ? Hd0 : Hp[pp][k - 1]) + sub[k].get(u);
+            const int XL = k == 0 ? XL0 : Xo[k - 1];
+            if (k == 0) Hd0 = HL;
+            if (!MK) {
+                const int H = min(min(M, XL), Yc[k]);
                 const int Ho = H + o;
-                if (FULL && i <= m) {
-                    int* f = p.full + 3 * ((long long)i * (p.n + 1) + jcol);
-                    f[0] = M; f[1] = XL; f[2] = Yc;
+                Xo[k] = min(XL, Ho);
+                Yc[k] = min(Yc[k], Ho);
+                Hp[pp][k] = H;
+            } else {
+                const int i = t - (lane * TD + k) + 1;
+                if (!colok[k]) {  // columns past n forward their left input (lane 63 carries column n)
+                    Hp[pp][k] = k == 0 ? HL : Hp[pp ^ 1][k - 1];
+                    Xo[k] = XL;
+                } else if (i >= 1) {
+                    const int H = min(min(M, XL), Yc[k]);
+                    const int Ho = H + o;
+                    if (FULL && i <= m) {
+                        int* f = p.full + 3 * ((long long)i * (p.n + 1) + jl + k + 1);
+                        f[0] = M; f[1] = XL; f[2] = Yc[k];
+                    }
+                    Xo[k] = min(XL, Ho);
+                    Yc[k] = min(Yc[k], Ho);
+                    Hp[pp][k] = H;
                 }
-                Xout = min(XL, Ho);
-                Yc = min(Yc, Ho);
-                Hout = H;
             }
         }
     };
@@ -1092,62 +1119,65 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
             clk0 = __builtin_amdgcn_s_memtime();
         }
         if (dbg && c == nch / 2) stamp1 = __builtin_amdgcn_s_memrealtime();
-        // ring slots of the rows this chunk publishes (t0-63 .. t0-48) must be free
-        wait_ge(cons(w + 1), RING, outfree, t0 - 47, 1);
+        // ring slots of the rows this chunk publishes (t0-64TD+1 .. t0-64TD+16) must be free
+        wait_ge(cons(w + 1), RING, outfree, t0 - 64 * TD + 17, 1);
         // the next chunk's profile values (rows up to t0+32 for lane 0)
         wait_ge(&cnt[CI_PRODQ], 0, qavail, t0 + 2 * FROWS, 2);
-        QPack<QT> subn;
-        subn.load_unaligned(qcol + (((unsigned)(t0 + FROWS - lane)) & qmask));
+        QPack<QT> subn[TD];
+#pragma unroll
+        for (int k = 0; k < TD; k++)
+            subn[k].load_unaligned(qcol[k] + (((unsigned)(t0 + FROWS - (lane * TD + k))) & qmask));
         auto sub_chunks = [&](auto MASKED) {
-            constexpr bool MK = decltype(MASKED)::value;
 #pragma unroll
             for (int sc = 0; sc < FROWS / 4; sc++) {
                 const int r0 = __builtin_amdgcn_readfirstlane(t0 + 4 * sc);  // steps r0 .. r0+3: lane 0 rows r0+1 .. r0+4
-                int eh[4] = {e01.x, e01.z, e23.x, e23.z};
-                int ex[4] = {e01.y, e01.w, e23.y, e23.w};
-                int4 n01, n23;
-                int oH[4], oX[4];
-                // left edges two sub-chunks ahead: rows r0+9 .. r0+12 (slots r0+8 .. r0+11)
-                wait_ge(prod(w), 0, avail, r0 + 12, 0);
+                // this sub-chunk's edges (read a sub-chunk ago) and the next one's (FROWS / 4 is even)
+                const int4& C01 = (sc & 1) ? B01 : A01;
+                const int4& C23 = (sc & 1) ? B23 : A23;
+                int4& N01 = (sc & 1) ? A01 : B01;
+                int4& N23 = (sc & 1) ? A23 : B23;
+                const int eh[4] = {C01.x, C01.z, C23.x, C23.z};
+                const int ex[4] = {C01.y, C01.w, C23.y, C23.w};
+                // left edges one sub-chunk ahead: rows r0+5 .. r0+8 (slots r0+4 .. r0+7)
+                wait_ge(prod(w), 0, avail, r0 + 8, 0);
                 {
-                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 8) & RMASK));
-                    n01 = e4[0];
-                    n23 = e4[1];
+                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 4) & RMASK));
+                    N01 = e4[0];
+                    N23 = e4[1];
+                    pnext = *prod_in;
                 }
-                if constexpr (!MK) {
-                    constexpr int QB = (int)sizeof(QT);
-                    diag4_asm<QB == 2>(eh, ex, Hd, Hout, Xout, Yc, sub.w[(4 * sc * QB) >> 2],
-                                       sub.w[((4 * sc + 2) * QB) >> 2], o, oH, oX);
-                    Hd = eh[3];
-                } else {
+                int oH[4], oX[4];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        step(eh[u], ex[u], sub.get(4 * sc + u), true, r0 + u);
-                        oH[u] = Hout;
-                        oX[u] = Xout;
-                    }
+                for (int u = 0; u < 4; u++) {
+                    step(eh[u], ex[u], 4 * sc + u, r0 + u, MASKED);
+                    oH[u] = Hp[u & 1][TD - 1];
+                    oX[u] = Xo[TD - 1];
                 }
-                // lane 63 has rows r0-62 .. r0-59; it publishes the 4-slot-aligned group r0-63 .. r0-60
-                // (the first from the previous sub-chunk) so a group never straddles the ring's end;
-                // rows < 1 land in slots nobody reads before their real rows overwrite them
-                const int pr = r0 - 63;
+                // the counter read before the block has landed: no wait on the LDS here, nor at the
+                // next sub-chunk's check (used after the publish, whose LDS operations the compiler
+                // does not count, it would wait for every LDS operation in flight)
+                asm volatile("" : "+v"(pnext));  // keeps the counter's use (and its wait) after the block
+                avail = sgpr_u(max(avail, pnext));
+                // lane 63's last column has rows r0-64TD+2 .. r0-64TD+5; it publishes the 4-slot-aligned
+                // group r0-64TD+1 .. r0-64TD+4 (the first from the previous sub-chunk) so a group never
+                // straddles the ring's end; rows < 1 land in slots nobody reads before their real rows
+                // overwrite them
+                const int pr = r0 - 64 * TD + 1;
                 lds_publish(rout_lds + (unsigned)((pr - 1) & RMASK) * 8u, pc_lds, edgemask,
                             v4i{cH, cX, oH[0], oX[0]}, v4i{oH[1], oX[1], oH[2], oX[2]}, (unsigned)(r0 + 4),
                             (unsigned)max(pr + 3, 0));
                 cH = oH[3];
                 cX = oX[3];
-                e01 = f01;
-                e23 = f23;
-                f01 = n01;
-                f23 = n23;
             }
         };
-        if (FULL || partial || t0 < 64) sub_chunks(std::true_type{});
+        if (FULL || partial || t0 < 64 * TD) sub_chunks(std::true_type{});
         else sub_chunks(std::false_type{});
-        sub = subn;
+#pragma unroll
+        for (int k = 0; k < TD; k++) sub[k] = subn[k];
     }
-    // the last row lane 63 computed (row nch*16 - 63), then everything (rows past m are padding)
-    if (lane == 63) (ring + (w + 1) * RING)[(nch * FROWS - 64) & RMASK] = make_int2(cH, cX);
+    // the last row lane 63's last column computed (row nch*16 - 64TD + 1), then everything (rows
+    // past m are padding)
+    if (lane == 63) rout[(nch * FROWS - 64 * TD) & RMASK] = make_int2(cH, cX);
     if (lane == 0) __hip_atomic_store(prod(w + 1), rows_end, RLX, WGS);
     if (dbg && lane == 0) {
         unsigned long long* d = p.dbg + 8 * s;
@@ -1779,29 +1809,40 @@ size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows) {
     return (size_t)FILL_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + QMIRROR) * qbytes;
 }
 
-template <typename QT, int NWC, bool FULL, bool DBG = false>
+template <typename QT, int NWC, int TD, bool FULL, bool DBG = false>
 static void launch_diag_one(hipStream_t s, const FillArgs& p) {
-    if (!DBG && p.dbg != nullptr) return launch_diag_one<QT, NWC, FULL, true>(s, p);
+    if (!DBG && p.dbg != nullptr) return launch_diag_one<QT, NWC, TD, FULL, true>(s, p);
     static const long floor_env = [] {
         const char* e = getenv("GA_FILL_LDS_FLOOR");
         return e ? atol(e) : -1L;
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_diag_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
-    auto* fn = fill_diag_kernel<QT, NWC, FULL, DBG>;
+    auto* fn = fill_diag_kernel<QT, NWC, TD, FULL, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
 
-void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full) {
-    if (full) return launch_diag_one<int8_t, 4, true>(s, p);  // debug (the host allows int8 profiles only)
+template <int TD>
+static void launch_diag_td(hipStream_t s, const FillArgs& p, int qbytes) {
     if (p.nwc == 4) {
-        if (qbytes == 1) launch_diag_one<int8_t, 4, false>(s, p);
-        else launch_diag_one<int16_t, 4, false>(s, p);
+        if (qbytes == 1) launch_diag_one<int8_t, 4, TD, false>(s, p);
+        else launch_diag_one<int16_t, 4, TD, false>(s, p);
     } else {
-        if (qbytes == 1) launch_diag_one<int8_t, 8, false>(s, p);
-        else launch_diag_one<int16_t, 8, false>(s, p);
+        if (qbytes == 1) launch_diag_one<int8_t, 8, TD, false>(s, p);
+        else launch_diag_one<int16_t, 8, TD, false>(s, p);
     }
+}
+
+void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full) {
+    // debug FULL output: 4 compute waves, int8 profiles (the host allows no other)
+    if (full) {
+        if (p.cols_per_lane == 1) return launch_diag_one<int8_t, 4, 1, true>(s, p);
+        return launch_diag_one<int8_t, 4, 2, true>(s, p);
+    }
+    if (p.cols_per_lane == 4) launch_diag_td<4>(s, p, qbytes);
+    else if (p.cols_per_lane == 2) launch_diag_td<2>(s, p, qbytes);
+    else launch_diag_td<1>(s, p, qbytes);
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {

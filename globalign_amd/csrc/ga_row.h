@@ -151,17 +151,20 @@ __device__ __forceinline__ void blocked_row(int (&Hprev)[T], int (&Yc)[T], int e
     "v_min_i32 " OX ", " EX ", %[Ho]\n\t"                                                             \
     "v_min_i32 %[Y], %[Y], %[Ho]\n\t"
 
+// e0..e3 / x0..x3: the left edge (H', h1') of the block's four rows, taken by lane 0; the
+// registers are overwritten (the DPP shifts land in them), so the caller hands its read buffer
 template <bool Q16>
-__device__ __forceinline__ void diag4_asm(int (&eh)[4], int (&ex)[4], int Hd, int& H, int& X, int& Y, uint32_t q0,
-                                          uint32_t q1, int o, int (&oH)[4], int (&oX)[4]) {
+__device__ __forceinline__ void diag4_asm(int& e0, int& e1, int& e2, int& e3, int& x0, int& x1, int& x2, int& x3,
+                                          int Hd, int& H, int& X, int& Y, uint32_t q0, uint32_t q1, int o,
+                                          int (&oH)[4], int (&oX)[4]) {
     int M, Ho;
     if (!Q16) {
         asm volatile(GA_DIAG_STEP0("%[e0]", "%[x0]", "%[Hd]", "%[H]", "%[X]", "%[q0]", "BYTE_0", "%[h0]", "%[y0]")
                      GA_DIAG_STEP("%[e1]", "%[x1]", "%[e0]", "%[h0]", "%[y0]", "%[q0]", "BYTE_1", "%[h1]", "%[y1]")
                      GA_DIAG_STEP("%[e2]", "%[x2]", "%[e1]", "%[h1]", "%[y1]", "%[q0]", "BYTE_2", "%[h2]", "%[y2]")
                      GA_DIAG_STEP("%[e3]", "%[x3]", "%[e2]", "%[h2]", "%[y2]", "%[q0]", "BYTE_3", "%[h3]", "%[y3]")
-                     : [e0] "+v"(eh[0]), [e1] "+v"(eh[1]), [e2] "+v"(eh[2]), [e3] "+v"(eh[3]), [x0] "+v"(ex[0]),
-                       [x1] "+v"(ex[1]), [x2] "+v"(ex[2]), [x3] "+v"(ex[3]), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
+                     : [e0] "+v"(e0), [e1] "+v"(e1), [e2] "+v"(e2), [e3] "+v"(e3), [x0] "+v"(x0),
+                       [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
                        [h2] "=&v"(oH[2]), [h3] "=&v"(oH[3]), [y0] "=&v"(oX[0]), [y1] "=&v"(oX[1]), [y2] "=&v"(oX[2]),
                        [y3] "=&v"(oX[3]), [Y] "+v"(Y), [M] "=&v"(M), [Ho] "=&v"(Ho)
                      : [Hd] "v"(Hd), [H] "v"(H), [X] "v"(X), [q0] "v"(q0), [o] "s"(o));
@@ -170,8 +173,8 @@ __device__ __forceinline__ void diag4_asm(int (&eh)[4], int (&ex)[4], int Hd, in
                      GA_DIAG_STEP("%[e1]", "%[x1]", "%[e0]", "%[h0]", "%[y0]", "%[q0]", "WORD_1", "%[h1]", "%[y1]")
                      GA_DIAG_STEP("%[e2]", "%[x2]", "%[e1]", "%[h1]", "%[y1]", "%[q1]", "WORD_0", "%[h2]", "%[y2]")
                      GA_DIAG_STEP("%[e3]", "%[x3]", "%[e2]", "%[h2]", "%[y2]", "%[q1]", "WORD_1", "%[h3]", "%[y3]")
-                     : [e0] "+v"(eh[0]), [e1] "+v"(eh[1]), [e2] "+v"(eh[2]), [e3] "+v"(eh[3]), [x0] "+v"(ex[0]),
-                       [x1] "+v"(ex[1]), [x2] "+v"(ex[2]), [x3] "+v"(ex[3]), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
+                     : [e0] "+v"(e0), [e1] "+v"(e1), [e2] "+v"(e2), [e3] "+v"(e3), [x0] "+v"(x0),
+                       [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [h0] "=&v"(oH[0]), [h1] "=&v"(oH[1]),
                        [h2] "=&v"(oH[2]), [h3] "=&v"(oH[3]), [y0] "=&v"(oX[0]), [y1] "=&v"(oX[1]), [y2] "=&v"(oX[2]),
                        [y3] "=&v"(oX[3]), [Y] "+v"(Y), [M] "=&v"(M), [Ho] "=&v"(Ho)
                      : [Hd] "v"(Hd), [H] "v"(H), [X] "v"(X), [q0] "v"(q0), [q1] "v"(q1), [o] "s"(o));

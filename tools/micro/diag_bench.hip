@@ -26,7 +26,7 @@ __global__ void steps(long long* out, int* sink, int nsteps) {
             e01 = e[0];
             e23 = e[1];
         }
-        ga::diag4_asm<false>(eh, ex, Hd, H, X, Y, q, q, 5, oH, oX);
+        ga::diag4_asm<false>(eh[0], eh[1], eh[2], eh[3], ex[0], ex[1], ex[2], ex[3], Hd, H, X, Y, q, q, 5, oH, oX);
         Hd = eh[3];
         if (MODE >= 2 && lane == 63) {
             reinterpret_cast<int4*>(lds)[512 + (r & 255)] = make_int4(oH[0], oX[0], oH[1], oX[1]);
