@@ -186,7 +186,8 @@ void fill_entries(const uint8_t* acc, int64_t steps, RngTable& R) {
         for (int half = 0; half < 2; half++) {
             const uint8_t* qq = r + 9 * half;
             const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
-            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 16 * half);
+            // level of rank set S at bits 2S+1+14*half (ga_kernels.hip, walk layout)
+            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 1 + 14 * half);
         }
         R.tab[st] = e;
     }

@@ -981,7 +981,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                     if (r <= hi) {
                         const int2 e = rout[(r - 1) & RMASK];
                         g_st64(dst + r, e);
-                        if (last_slab && r == (unsigned)m) p.out_last[0] = e.x;  // H'(m, n): the cost
+                        // H'(m, n): the cost (a partial last stripe's compute wave writes it)
+                        if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     if (lane == 0) {
@@ -1016,7 +1017,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     const int s = g * NWC + w;
     const int j0 = s * 64 * TD;
     const int jl = j0 + lane * TD;                // this lane: columns jl+1 .. jl+TD
-    const bool partial = j0 + 64 * TD > p.n;      // uniform: the stripe holding column n, when it is not whole
+    // the stripe holding column n, when it is not whole: its columns past n compute garbage and the
+    // lane holding column n reports H'(m, n) itself (column c of the stripe has row m at step m+c-1)
+    const bool partial = j0 + 64 * TD > p.n;
+    const int cn = p.n - 1 - j0;
+    const int tm = partial ? m - 1 + cn : -1;
+    int Hm = 0;
     const QT* qcol[TD];
     bool colok[TD];
     // per column: H' of the last two steps (by step parity), the h1' it passes right, h2'
@@ -1094,7 +1100,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                 Hp[pp][k] = H;
             } else {
                 const int i = t - (lane * TD + k) + 1;
-                if (!colok[k]) {  // columns past n forward their left input (lane 63 carries column n)
+                if (!colok[k]) {  // columns past n forward their left input (the FULL debug output)
                     Hp[pp][k] = k == 0 ? HL : Hp[pp ^ 1][k - 1];
                     Xo[k] = XL;
                 } else if (i >= 1) {
@@ -1152,6 +1158,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                     step(eh[u], ex[u], 4 * sc + u, r0 + u, MASKED);
                     oH[u] = Hp[u & 1][TD - 1];
                     oX[u] = Xo[TD - 1];
+                    if (tm == r0 + u) {  // uniform, once per stripe
+#pragma unroll
+                        for (int k = 0; k < TD; k++)
+                            if (cn % TD == k) Hm = Hp[u & 1][k];
+                    }
                 }
                 // the counter read before the block has landed: no wait on the LDS here, nor at the
                 // next sub-chunk's check (used after the publish, whose LDS operations the compiler
@@ -1170,7 +1181,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                 cX = oX[3];
             }
         };
-        if (FULL || partial || t0 < 64 * TD) sub_chunks(std::true_type{});
+        if (FULL || t0 < 64 * TD) sub_chunks(std::true_type{});
         else sub_chunks(std::false_type{});
 #pragma unroll
         for (int k = 0; k < TD; k++) sub[k] = subn[k];
@@ -1179,6 +1190,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     // past m are padding)
     if (lane == 63) rout[(nch * FROWS - 64 * TD) & RMASK] = make_int2(cH, cX);
     if (lane == 0) __hip_atomic_store(prod(w + 1), rows_end, RLX, WGS);
+    if (partial && lane == cn / TD) p.out_last[0] = Hm;
     if (dbg && lane == 0) {
         unsigned long long* d = p.dbg + 8 * s;
         d[0] = stamp0;
@@ -1206,10 +1218,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
 // the mostly-sleeping helper only.
 //
 // A cached cell is a u16 of three 5-bit shifts, one per entering level L:
-// sh_L = 2*S_L + 16*(a_i != b_j), S_L the rank set of sets_from_code.  The
-// host table entry of dispatch D holds, at bits sh..sh+1, the level the
-// reference's random.choice picks for that set (match half at 2S, mismatch
-// half at 16+2S), so a step is lvl = (tab >> sh_L) & 3.
+// sh_L = 2*S_L - 2 + 14*(a_i != b_j), S_L (1..7) the rank set of sets_from_code.
+// The host table entry of dispatch D holds, at bits sh+3..sh+4, the level the
+// reference's random.choice picks for that set (match half at 2S+1, mismatch
+// half at 15+2S), so a step's level comes out already times 8 (the bit offset
+// of the next entering level's field): L8 = (tab >> sh_L) & 0x18.
 //
 // Wave 0 walks with scalar code only, in groups of 4 steps: each group issues
 // the LDS read of the 8x8 window anchored at its first cell (lane r*8+c =
@@ -1245,9 +1258,11 @@ __device__ __forceinline__ int sets_from_code(unsigned code, int CB, int o) {
 }
 
 // three 5-bit table shifts (one per entering level) from the rank sets and a_i == b_j
+// (an empty set -- cells outside the matrix, never walked -- wraps to 30: level 0)
 __device__ __forceinline__ unsigned cell_shifts(int sets, bool am) {
-    const unsigned mm = am ? 0u : 16u;
-    const unsigned f0 = 2u * (sets & 7) + mm, f1 = 2u * ((sets >> 3) & 7) + mm, f2 = 2u * ((sets >> 6) & 7) + mm;
+    const unsigned mm = am ? 0u : 14u;
+    const unsigned f0 = (2u * (sets & 7) - 2u + mm) & 31u, f1 = (2u * ((sets >> 3) & 7) - 2u + mm) & 31u,
+                   f2 = (2u * ((sets >> 6) & 7) - 2u + mm) & 31u;
     return f0 | (f1 << 5) | (f2 << 10);
 }
 
@@ -1576,9 +1591,9 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                 const long long M = vv[0], X = vv[1], Y = vv[2];
                 S = L == 0 ? argmin3(M, X, Y) : L == 1 ? argmin3(M + o, X, Y + o) : argmin3(M + o, X + o, Y);
             }
-            sh = (unsigned)sgpr((int)(2u * S + (w.a[pa] == w.b[pb] ? 0u : 16u)));
+            sh = (unsigned)sgpr((int)(2u * S - 2u + (w.a[pa] == w.b[pb] ? 0u : 14u)));
         }
-        const int lvl = (int)((tab >> sh) & 3u);
+        const int lvl = (int)((tab >> (sh + 3u)) & 3u);
         uint8_t* ob = ops_byte(D);
         *ob = (uint8_t)(((D & 3) ? *ob : 0) | (lvl << (6 - 2 * (D & 3))));
         D++;
@@ -1654,14 +1669,17 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
             __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
             const unsigned t[4] = {(unsigned)sgpr((int)tc.x), (unsigned)sgpr((int)tc.y), (unsigned)sgpr((int)tc.z),
                                    (unsigned)sgpr((int)tc.w)};
-            unsigned idx = rel, mv = 0;
+            unsigned ix = rel, mv = 0;  // ix: the readlane index (only its low 6 bits count: unmasked sums)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)(idx + mv));
-                const unsigned lvl = (t[k] >> ((v >> L8) & 31u)) & 3u;
-                ops = ops * 4u + lvl;
-                L8 = lvl << 3;
-                mv += (0x080109u >> L8) & 0xffu;  // diag 9, left 1, up 8
+                const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)ix);
+                // the chosen level comes out as the next field's bit offset (lvl * 8): two dependent
+                // scalar ops fewer per step than extracting lvl and scaling it
+                L8 = (t[k] >> ((v >> L8) & 31u)) & 0x18u;
+                ops = ops * 4u + (L8 >> 3);
+                const unsigned dm = 0x080109u >> L8;  // low byte: diag 9, left 1, up 8
+                ix += dm;
+                mv += dm & 0xffu;
                 if (CHECK) {
                     if ((int)(mv >> 3) == i || (int)(mv & 7u) == j) {
                         i -= (int)(mv >> 3);

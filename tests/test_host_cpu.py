@@ -51,7 +51,7 @@ def test_tiebreak_table_matches_cpython(lib, seed, steps):
         e = 0
         for half in (0, 1):
             for S in range(1, 8):
-                e |= lv[half][S] << (2 * S + 16 * half)
+                e |= lv[half][S] << (2 * S + 1 + 14 * half)
         want.append(e)
         states.append(random.getstate())
     for D in sorted({0, 1, steps // 2, steps}):

@@ -48,6 +48,10 @@ out = {
     "row_ns_median": float(np.median(step_ns)),
     "first_half_vs_second_half": float(np.median((mid - start) / np.maximum(end - mid, 1e-9))),
     "start_us_samples": [float(x) for x in start[:: max(1, ns // 12)]],
+    "latest_ends": [[int(k), round(float(start[k]), 1), round(float(end[k]), 1)] for k in np.argsort(end)[-5:]],
+    "max_start_us": float(start.max()),
+    "row_ns_samples": [round(float(x), 1) for x in step_ns[:: max(1, ns // 12)]],
+    "wait_frac_samples": [round(float(x), 3) for x in (st[:: max(1, ns // 12), 4] / np.maximum(st[:: max(1, ns // 12), 3], 1))],
     # shader clocks (s_memtime) over the same span as end - start: the in-kernel clock and cycles per row
     "clock_ghz_median": float(np.median(st[:, 3] / np.maximum(dur * 1e3, 1e-9))),
     "cycles_per_row_median": float(np.median(st[:, 3] / m)),
@@ -72,5 +76,8 @@ if tb:
     L.ga_debug_walk.argtypes = [C.c_void_p, C.c_void_p]
     w2 = np.zeros(8, dtype=np.int32)
     L.ga_debug_walk(eng._h, w2.ctypes.data)
-    out["walk"] = dict(eng.timings(), tile_wait_sleeps=int(w2[0]), tiles=int(w2[1]))
+    out["walk"] = dict(eng.timings(), tile_wait_sleeps=int(w2[0]), tiles=int(w2[1]),
+                       tile_wait_us=float(w2[2]) / 100.0, ring_wait_us=float(w2[3]) / 100.0,
+                       walker_us=float(w2[4]) / 100.0, walker_cycles=int(w2[5]), load_ticks=int(w2[6]),
+                       loads=int(w2[7]))
 print(json.dumps(out))

@@ -16,6 +16,12 @@ __global__ void chain(long long* out, int* sink, int n) {
             L8 = lvl << 3;
             idx += (0x080109u >> L8) & 0xffu;
             acc += lvl;
+        } else if (V == 3) {  // table pre-shifted by 3 in 64 bits: the level's bit offset comes out masked
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)(idx & 63));
+            const unsigned long long t64 = (unsigned long long)t << 3;
+            L8 = (unsigned)(t64 >> ((v >> L8) & 63u)) & 0x18u;
+            idx += 0x080109u >> L8;
+            acc += L8;
         } else if (V == 1) {  // readlane -> one scalar add -> readlane
             const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)(idx & 63));
             idx += v;
@@ -49,6 +55,7 @@ double run(F f) {
 int main() {
     printf("walker step (readlane + 8 SALU): %.1f cyc\n", run(chain<0>));
     printf("readlane -> s_add -> readlane : %.1f cyc\n", run(chain<1>));
+    printf("walker step, 64-bit table     : %.1f cyc\n", run(chain<3>));
     printf("8 dependent SALU ops          : %.1f cyc\n", run(chain<2>));
     return 0;
 }
