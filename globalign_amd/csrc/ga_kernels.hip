@@ -1669,25 +1669,30 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
             __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
             const unsigned t[4] = {(unsigned)sgpr((int)tc.x), (unsigned)sgpr((int)tc.y), (unsigned)sgpr((int)tc.z),
                                    (unsigned)sgpr((int)tc.w)};
-            unsigned ix = rel, mv = 0;  // ix: the readlane index (only its low 6 bits count: unmasked sums)
+            // ix: the readlane index.  Only its low 6 bits count, so the moves go in unmasked; its low
+            // byte is rel + the group's moves (diag 9, left 1, up 8: at most 4 rows and 4 columns).
+            // A: the group's levels times 8, base 4.  (The walker is issue-bound: ~7 scalar ops a step.)
+            unsigned ix = rel, A = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)ix);
                 // the chosen level comes out as the next field's bit offset (lvl * 8): two dependent
                 // scalar ops fewer per step than extracting lvl and scaling it
                 L8 = (t[k] >> ((v >> L8) & 31u)) & 0x18u;
-                ops = ops * 4u + (L8 >> 3);
-                const unsigned dm = 0x080109u >> L8;  // low byte: diag 9, left 1, up 8
-                ix += dm;
-                mv += dm & 0xffu;
+                A = A * 4u + L8;
+                ix += 0x080109u >> L8;
                 if (CHECK) {
+                    const unsigned mv = (ix - rel) & 0xffu;
                     if ((int)(mv >> 3) == i || (int)(mv & 7u) == j) {
                         i -= (int)(mv >> 3);
                         j -= (int)(mv & 7u);
+                        ops = (ops << (2 * (k + 1))) | (A >> 3);
                         return k + 1;
                     }
                 }
             }
+            ops = (ops << 8) | (A >> 3);
+            const unsigned mv = (ix - rel) & 0xffu;
             i -= (int)(mv >> 3);
             j -= (int)(mv & 7u);
             rel = mv;
