@@ -101,3 +101,13 @@ def test_gpu_slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
     big = (tab.max_cost + 1) * max(m, n)
     row0, col0 = core.boundary(tab, a, b, goc, big)
     assert int(r["cost"]) == int(min(core.fill_score_parallel(tab, a, b, goc, row0, col0, 4)))
+
+
+@pytest.mark.parametrize("td", [1, 2])
+def test_gpu_slabs_score_only_diag_match_oracle(td, monkeypatch, tmp_path):
+    """The anti-diagonal fill (chosen automatically for the tall N = 8 slabs of C4) in slab mode: the left
+    edge from the neighbour rank's progress word, the right edge out to it, the cost from the last rank."""
+    monkeypatch.setenv("GA_FILL_MODE", "diag")
+    monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
+    test_gpu_slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
+    test_gpu_slabs_score_only_match_oracle(3, 12_000, 2_000 + 5, 47 + td, 2048, tmp_path)
