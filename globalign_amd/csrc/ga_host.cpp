@@ -332,7 +332,8 @@ int check_ctx(ga_ctx* c) {
 // Blocked stripes pay the wave scan, the edge traffic and the control once per 64*T cells, but
 // leave fewer stripes (waves) to fill the chip and lengthen each row's dependent chain.  A
 // workgroup chains 4 waves (one per SIMD) when every stripe gets a wave that way, else 8.
-void set_stripes(ga_ctx* c, int T_req, bool tb, bool full) {
+void set_stripes(ga_ctx* c, int T_req, bool tb, bool full, int64_t ncols = -1) {
+    const int64_t ncol = ncols < 0 ? c->n : ncols;  // a traceback band may cover a prefix of the columns
     const int64_t simds = 4 * (int64_t)c->num_cu;
     // register budget (no spills, see the code objects' vgpr_spill_count): the FULL debug output is
     // T == 1 only; traceback words T <= 2; score only T <= 8 with an int8 profile, 4 with int16
@@ -344,7 +345,7 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full) {
         // the widest stripes that still leave >= 1.5 waves per SIMD (measured: 1M columns score
         // only T = 8 > 4 > 2 > 1; 100k columns with traceback T = 1 > 2 > 4)
         for (int t = cap; t > 1; t /= 2)
-            if ((c->n + 64 * t - 1) / (64 * t) * 2 >= 3 * simds) {
+            if ((ncol + 64 * t - 1) / (64 * t) * 2 >= 3 * simds) {
                 T = t;
                 break;
             }
@@ -353,7 +354,7 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full) {
     // takes the edge from any lane)
     while (T > 1 && c->col0 + c->n < c->n_global && c->n % (64 * T) != 0) T /= 2;
     c->T = T;
-    c->nstripes = (int)((c->n + 64 * T - 1) / (64 * T));
+    c->nstripes = (int)((ncol + 64 * T - 1) / (64 * T));
     c->nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : c->nstripes <= 4 * c->num_cu ? 4 : 8;
     c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
 }
@@ -460,6 +461,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
 // top row from a checkpoint (nullptr: row 0), no boundary pass; or the checkpointing pass itself.
 struct Band {
     int64_t r0 = 0, mb = 0;
+    int64_t nc = 0;             // columns 1..nc only (0: all): the walk enters the band at column nc
     const int2* top = nullptr;  // (H', h2') of row r0, [n+1] (column 0 = the left edge's corner)
     bool band = false;          // fill rows r0+1 .. r0+mb only (the boundary is already computed)
     int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
@@ -471,7 +473,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
     const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
     const bool full = (flags & GA_FILL_FULL) != 0;
-    const int64_t m = bd.band ? bd.mb : c->m, n = c->n;
+    const int64_t m = bd.band ? bd.mb : c->m, n = bd.band && bd.nc > 0 ? bd.nc : c->n;
     // 16-row chunks; CB 16-byte words per lane per chunk (ga_device.h)
     c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
     // score only: the anti-diagonal kernel (64-column stripes) when asked for and its profile
@@ -486,7 +488,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && m >= 6 * n && (n + 63) / 64 <= 8 * (int64_t)c->num_cu;
     if ((!tb || (full && c->qbytes == 1)) && (c->diag_req == 2 || auto_diag) && bd.ckpt == nullptr) {
         const int td = full ? std::min(std::max(c->diag_T_req, 1), 2) : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req : 1;
-        set_stripes(c, td, false, false);
+        set_stripes(c, td, false, false, n);
         if (full) {  // the debug FULL variant is built for 4 compute waves
             c->nwc = 4;
             c->nslabs = (c->nstripes + 3) / 4;
@@ -497,7 +499,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     }
     if (!c->diag) {
         qrows = c->qrows;
-        set_stripes(c, c->T_req, tb, full);
+        set_stripes(c, c->T_req, tb, full, n);
     }
     // traceback words cover T 64-column stripes per fill stripe
     if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
@@ -801,6 +803,10 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
         bd.band = true;
         bd.r0 = b * Bh;
         bd.mb = b == nb - 1 ? m - bd.r0 : Bh;
+        // the path only moves up and left: this band's cells right of the column where the walk
+        // enters it are never read, so the band fills columns 1..j only (on a diagonal-ish path
+        // about half the refill work of full-width bands)
+        bd.nc = st.j;
         if (b > 0) {
             int2* row = ck + (size_t)(b - 1) * (n + 1);
             // column 0 of the checkpoint row: the left edge's corner H'(r0, 0)
