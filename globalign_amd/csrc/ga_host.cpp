@@ -481,11 +481,13 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // (its query-profile ring deeper than a workgroup's skew: NWC stripes x 64*TD steps)
     int qrows = c->qrows;
     c->diag = false;
-    // automatic: score-only fills of tall, narrow problems (m >= 6 n, <= 8 stripes per CU: the
-    // N = 8 slab of C4, 1M x 125k, fills in 95 ms against 107 ms for the row scan; the row scan wins
-    // on square shapes, where the anti-diagonal skew of 64 steps per stripe costs more,
-    // profiles/r01/diag_sweep.txt)
-    const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && m >= 6 * n && (n + 63) / 64 <= 8 * (int64_t)c->num_cu;
+    // automatic: score-only fills of tall, narrow problems on one GPU (m >= 6 n, <= 8 stripes per CU:
+    // 1M x 125k fills in 95 ms against 107 ms for the row scan; the row scan wins on square shapes,
+    // where the anti-diagonal skew of 64 steps per stripe costs more, profiles/r01/diag_sweep.txt).
+    // Not for a slab of a multi-GPU fill: there the next rank starts when this one's last stripe
+    // does, and that start (the ramp) is 15 ms for the anti-diagonal fill against 3.6 ms.
+    const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && !c->slab && m >= 6 * n &&
+                           (n + 63) / 64 <= 8 * (int64_t)c->num_cu;
     if ((!tb || (full && c->qbytes == 1)) && (c->diag_req == 2 || auto_diag) && bd.ckpt == nullptr) {
         const int td = full ? std::min(std::max(c->diag_T_req, 1), 2) : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req : 1;
         set_stripes(c, td, false, false, n);

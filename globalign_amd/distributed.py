@@ -47,9 +47,17 @@ def slab_bounds(n, world, align=256):
     return edges
 
 
-def bands(m, band):
-    """Row bands (r0, r1), 1-based inclusive, covering rows 1..m."""
-    return [(r0, min(m, r0 + band - 1)) for r0 in range(1, m + 1, band)]
+def bands(m, band, first=512):
+    """Row bands (r0, r1), 1-based inclusive, covering rows 1..m: `first` rows, then doubling up to `band`.
+
+    The next rank's fill starts when the first band arrives, so the first bands are short (the
+    pipeline's start-up per slab boundary: one short band instead of one `band`-row band)."""
+    out, r0, h = [], 1, max(1, min(first, band))
+    while r0 <= m:
+        out.append((r0, min(m, r0 + h - 1)))
+        r0 += h
+        h = min(2 * h, band)
+    return out
 
 
 class Links:

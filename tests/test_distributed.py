@@ -243,3 +243,8 @@ def test_slab_bounds_and_bands():
         slab_bounds(3, 4)
     bl = bands(1000, 256)
     assert bl[0] == (1, 256) and bl[-1] == (769, 1000) and len(bl) == 4
+    # short first bands, doubling up to the band height; contiguous cover of 1..m
+    bl = bands(100_000, 8192)
+    assert bl[0] == (1, 512) and bl[1] == (513, 1536) and bl[-1][1] == 100_000
+    assert all(b[0] == a[1] + 1 for a, b in zip(bl, bl[1:])) and max(r1 - r0 + 1 for r0, r1 in bl) == 8192
+    assert bands(7, 8192) == [(1, 7)]
