@@ -1258,12 +1258,12 @@ __device__ __forceinline__ int sets_from_code(unsigned code, int CB, int o) {
 }
 
 // three 5-bit table shifts (one per entering level) from the rank sets and a_i == b_j
-// (an empty set -- cells outside the matrix, never walked -- wraps to 30: level 0)
+// (every walked cell has three non-empty sets; an empty one -- cells outside the matrix, never
+// walked -- borrows from the next field, which is then garbage nobody reads)
 __device__ __forceinline__ unsigned cell_shifts(int sets, bool am) {
-    const unsigned mm = am ? 0u : 14u;
-    const unsigned f0 = (2u * (sets & 7) - 2u + mm) & 31u, f1 = (2u * ((sets >> 3) & 7) - 2u + mm) & 31u,
-                   f2 = (2u * ((sets >> 6) & 7) - 2u + mm) & 31u;
-    return f0 | (f1 << 5) | (f2 << 10);
+    const unsigned u = (unsigned)sets;
+    const unsigned s2 = ((u & 7u) | ((u & 0x38u) << 2) | ((u & 0x1c0u) << 4)) << 1;  // 2*S_L at bits 0/5/10
+    return s2 + (am ? 0u - 2u * 0x421u : 12u * 0x421u);                            // + (mm - 2) per field
 }
 
 __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, int i, int j) {
