@@ -1364,10 +1364,10 @@ constexpr int WALK_DBG = 8192;  // tile-need records kept by the diagnostic walk
 
 __device__ __forceinline__ int sgpr(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Waves: 0 walker, 4 ring helper, 8 idle (so the walker's SIMD runs nothing
-// else), the other nine load tiles.
-constexpr int WALK_WAVES = 12;
-constexpr int NLOAD = 9;
+// Waves: 0 walker, 4 ring helper, 8 L2 prefetcher, 12 idle (the walker's SIMD runs
+// nothing busy), the other twelve load tiles (three per SIMD).
+constexpr int WALK_WAVES = 16;
+constexpr int NLOAD = 12;
 
 __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
     const int dti = (cur >> 16) - ti, dtj = (cur & 0xffff) - tj;
@@ -1459,24 +1459,26 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
 
     if (wave > 0) {
         // ---------------- loader pool: slot ownership ----------------
-        // Loader k (k < 8) owns torus slots k and k+8: each slot has one writer, so no claim
-        // protocol is needed, and the tiles the walker needs next (offsets (1,0), (0,1), (1,1)
-        // of its tile) always sit in different slots, so different loaders fetch them at once.
+        // Loader k (k < 12) owns torus slot k, loaders 0..3 also slot k+12: each slot has one
+        // writer, so no claim protocol is needed, and the tiles the walker needs next (offsets
+        // (1,0), (0,1), (1,1) of its tile) sit in different slots.
         // Before overwriting a slot the owner invalidates its tag and re-reads the current tile:
         // a tile the walker may still read (inside its 4x4 block) is never overwritten, since
         // the walker publishes its tile before it checks a tag.
-        const int li = wave - 1 - (wave > 4) - (wave > 8);
-        if (li >= 8) return;
+        if (wave == 12) return;
+        const int li = wave - 1 - (wave > 4) - (wave > 8) - (wave > 12);  // 0 .. NLOAD-1
+        const int nown = li < NSLOT - NLOAD ? 2 : 1;
         while (!sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS))) {
             const int cur = sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS));
             bool did = false;
             if (cur >= 0) {
                 const int ti = cur >> 16, tj = cur & 0xffff;
                 // the block tile of each owned slot (the one congruent to it, at offsets 0..3)
-                int cand[2], dist[2];
+                int cand[2] = {-1, -1}, dist[2] = {1 << 20, 1 << 20};
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
-                    const int sl = li + 8 * q, sr = sl >> 2, sc = sl & 3;
+                    if (q >= nown) break;
+                    const int sl = li + NLOAD * q, sr = sl >> 2, sc = sl & 3;
                     const int di = (ti - sr) & (TB4 - 1), dj = (tj - sc) & (TB4 - 1);
                     cand[q] = (ti - di < 0 || tj - dj < 0) ? -1 : (((ti - di) << 16) | (tj - dj));
                     dist[q] = di + dj;
@@ -1486,7 +1488,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                     const int q = qq ^ first_q;
                     const int tg = cand[q];
                     if (tg < 0) continue;
-                    const int sl = li + 8 * q, tti = tg >> 16, ttj = tg & 0xffff;
+                    const int sl = li + NLOAD * q, tti = tg >> 16, ttj = tg & 0xffff;
                     if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
                     if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_SEQ_CST, WGS);
                     if (!in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
