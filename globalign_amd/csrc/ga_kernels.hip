@@ -1289,7 +1289,7 @@ __device__ __forceinline__ int torus_of(int i, int j) { return ((i - 1) & (TP - 
 // traceback stream (the general path; one-byte words use load_tile_b1).
 template <int CB>
 __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
-                          int lane) {
+                          const uint8_t* lutF, int lane) {
     uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT;
     constexpr int SPC = 16 / CB;
     constexpr int KW = TT / SPC;
@@ -1314,7 +1314,16 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, ui
             unsigned code = wd[(u * CB) >> 2] >> ((u * CB * 8) & 31);
             if (CB == 1) code &= 0xffu;
             else if (CB == 2) code &= 0xffffu;
-            dst[r * TP + lane] = (uint16_t)cell_shifts(sets_from_code(code, CB, w.o), sa[r] == bj);
+            if constexpr (CB == 2) {
+                // two-byte words: each 7-bit field's (== 0, <= o, >= o) flags from lutF, the three
+                // levels' shifts from lut (zM bit, both fields' flags, a_i == b_j): the general decode
+                // below made the C5 walk wait on tile loads (9.7 us a tile)
+                const unsigned idx = ((code >> 14) & 1u) | ((unsigned)lutF[code & 127u] << 1) |
+                                     ((unsigned)lutF[(code >> 7) & 127u] << 4) | (sa[r] == bj ? 128u : 0u);
+                dst[r * TP + lane] = lut[idx];
+            } else {
+                dst[r * TP + lane] = (uint16_t)cell_shifts(sets_from_code(code, CB, w.o), sa[r] == bj);
+            }
         }
     }
 }
@@ -1380,6 +1389,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     __shared__ __attribute__((aligned(16))) uint32_t rngbuf[RB];
     __shared__ uint32_t opsbuf[RB / 16];
     __shared__ uint16_t lut[256];
+    __shared__ uint8_t lutF[128];
     __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD][TT];
     __shared__ int tag[NSLOT];
     __shared__ int rtag[4];
@@ -1396,6 +1406,21 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; }
     if (CB == 1 && threadIdx.x < 256)
         lut[threadIdx.x] = (uint16_t)cell_shifts(sets_from_code(threadIdx.x & 127u, 1, o), (threadIdx.x >> 7) != 0);
+    if (CB == 2 && threadIdx.x < 128) {
+        const int v = (int)threadIdx.x;
+        lutF[v] = (uint8_t)((v == 0) | ((v <= o) << 1) | ((v >= o) << 2));
+    }
+    if (CB == 2 && threadIdx.x < 256) {
+        // sets_from_code in terms of the flags: bit 0 the raw zM bit, bits 1-3 / 4-6 the (zero, le, ge)
+        // flags of the X / Y fields, bit 7 a_i == b_j
+        const unsigned x = threadIdx.x;
+        const unsigned zM = (x & 1u) ^ 1u, zX = (x >> 1) & 1u, leX = (x >> 2) & 1u, geX = (x >> 3) & 1u;
+        const unsigned zY = (x >> 4) & 1u, leY = (x >> 5) & 1u, geY = (x >> 6) & 1u;
+        const unsigned S0 = zM | (zX << 1) | (zY << 2);
+        const unsigned S1 = (zM & geX) | (leX << 1) | ((zY & geX) << 2);
+        const unsigned S2 = (zM & geY) | ((zX & geY) << 1) | (leY << 2);
+        lut[x] = (uint16_t)cell_shifts((int)(S0 | (S1 << 3) | (S2 << 6)), (x >> 7) != 0);
+    }
     __syncthreads();
 
     if (wave == 8) {
@@ -1494,7 +1519,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                     if (!in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                     if (CB == 1) load_tile_b1(w, tti, ttj, torus, sa[li], lut, lane);
-                    else load_tile<CB>(w, tti, ttj, torus, sa[li], lut, lane);
+                    else load_tile<CB>(w, tti, ttj, torus, sa[li], lut, lutF, lane);
                     if (lane == 0) {
                         atomicAdd(&load_ticks, __builtin_amdgcn_s_memrealtime() - t0);
                         atomicAdd(&load_count, 1);
