@@ -1665,8 +1665,8 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
             const unsigned r = (unsigned)(pi - 1 - lr) & (TP - 1), c = (unsigned)(pj - 1 - lc) & (TP - 1);
             return torus[r * TP + c];
         };
-        // widen a window cell when its group starts: the empty asm keeps the compiler from pulling the
-        // widening (and so the wait for the LDS read) back into the group that issued the read
+        // widen a window cell (at the last step of the group that issued its read): the empty asm keeps
+        // the compiler from pulling the widening (and so the wait for the LDS read) further forward
         auto widen = [](int raw) -> int {
             asm volatile("" : "+v"(raw));
             const unsigned u = (unsigned)raw;
@@ -1680,6 +1680,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
         }
         verify(i, j);
         int wnext = window(i, j);    // anchored at the walk's current cell
+        int wcw = widen(wnext);      // the next group's window, widened (off the next group's chain)
         uint4 tnext = tabs(D);
         unsigned rel = 0;            // offset of the current cell from wnext's anchor (di*8 + dj)
         unsigned L8 = 8u * L;        // bit offset of the entering level's field in a window cell
@@ -1689,7 +1690,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
         // CHECK: stop at the matrix edge; returns the steps taken when the walk ended, else 0.
         auto group = [&](auto check_tag, int gd) -> int {  // gd: dispatch of the group's first step
             constexpr bool CHECK = decltype(check_tag)::value;
-            const int wcur = widen(wnext);
+            const int wcur = wcw;
             const uint4 tc = tnext;
             wnext = window(i, j);
             tnext = tabs(gd + 4);
@@ -1703,6 +1704,9 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)ix);
+                // widen the next group's window (read at this group's start) while the last step's
+                // scalar chain runs
+                if (k == 3) wcw = widen(wnext);
                 // the chosen level comes out as the next field's bit offset (lvl * 8): two dependent
                 // scalar ops fewer per step than extracting lvl and scaling it
                 L8 = (t[k] >> ((v >> L8) & 31u)) & 0x18u;
