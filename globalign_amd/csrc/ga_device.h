@@ -14,6 +14,9 @@ constexpr int FROWS = 16;        // rows per fill chunk (one 16-byte traceback s
 #define GA_GOUT 16
 #endif
 constexpr int GOUT = GA_GOUT;    // rows per cross-workgroup publish
+// an unwritten row of the workgroup hand-off buffer (memset byte 0x80): no H' reaches it (the
+// int32 range guard keeps every value below INT32_MAX / 4 in magnitude)
+constexpr int HAND_SENT = (int)0x80808080u;
 constexpr int FILL_LDS_MIN = 82 * 1024;  // > 80 KB: one fill workgroup per CU
 
 struct FillArgs {

@@ -506,6 +506,9 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // traceback words cover T 64-column stripes per fill stripe
     if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
     HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
+    // workgroup hand-off rows read by a successor start as ga::HAND_SENT (bytes 0x80)
+    if (c->nslabs > 1)
+        HIPCHK(hipMemsetAsync(c->hand.p, 0x80, sizeof(int2) * (size_t)(c->nslabs - 1) * (m + 1), c->stream));
     HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
     if (full) {
         if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");

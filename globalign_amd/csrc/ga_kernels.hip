@@ -420,6 +420,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         const int2* rout = ring + nlive * RING;
         const int K = p.K;
         const int h00 = p.top[g * NWC * 64 * T].x;  // H'(0, left edge of this workgroup's columns)
+        // workgroup hand-offs poll the rows themselves (HAND_SENT until written, ga_device.h);
+        // only the slab's own right edge out to another GPU keeps the progress word
+        const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
+        int hlast = h00;  // H' of row in_next of the left edge
         unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
         while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
@@ -443,7 +447,26 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                     moved = true;
                 }
             }
-            if (in_next < (unsigned)m) {
+            if (in_next < (unsigned)m && in_sent) {
+                // the contiguous written prefix of the next (up to) 64 rows, as far as ring 0 has space
+                const unsigned cap = min(min(lds_ld(&pc.cons(0)) + RING, (unsigned)m), in_next + 64);
+                if (cap > in_next) {
+                    const unsigned r = in_next + 1 + lane;
+                    const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
+                    const unsigned long long ok = __ballot(e1.x != HAND_SENT);
+                    const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;  // rows in_next+1 .. +k
+                    if (k > 0) {
+                        // H' of row r-1: the lane before (lane 0: the last row of the previous batch)
+                        const int h0 = __builtin_amdgcn_update_dpp(hlast, e1.x, 0x138, 0xf, 0xf, false);
+                        if (lane < (int)k) rin0[(r - 1) & RMASK] = make_int2(h0, e1.y - o);
+                        hlast = __builtin_amdgcn_readlane(e1.x, (int)k - 1);
+                        const unsigned hi = in_next + k;
+                        if (lane == 0) lds_st(&pc.prod(0), hi == (unsigned)m ? (unsigned)mpad : hi);
+                        in_next = hi;
+                        moved = true;
+                    }
+                }
+            } else if (in_next < (unsigned)m) {
                 // ring 0 slots are free below cons[0]
                 const unsigned space = lds_ld(&pc.cons(0)) + RING;
                 const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
@@ -472,13 +495,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                         g_st64(dst + r, make_int2(H, rout[(r - 1) & RMASK].y + o));
                         if (T == 1 && last_slab && r == (unsigned)m) p.out_last[0] = H;  // H'(m, n): the cost
                     }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) {
-                        g_st(p.hand_prog + g, hi);
-                        if (p.edge_prog != nullptr && last_slab)
-                            __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
-                        lds_st(&pc.cons(nlive), hi - 1u);
+                    if (!out_sent) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
+                    if (lane == 0) lds_st(&pc.cons(nlive), hi - 1u);
                     out_next = hi;
                     moved = true;
                 }
@@ -936,6 +957,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
         int2* rin0 = ring;
         const int2* rout = ring + nlive * RING;
         const int K = p.K;
+        const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);  // as in fill_kernel
         unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
         while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
@@ -960,7 +982,22 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                     moved = true;
                 }
             }
-            if (in_next < (unsigned)m) {
+            if (in_next < (unsigned)m && in_sent) {
+                const unsigned cap = min(min(lds_ld(cons(0)) + RING, (unsigned)m), in_next + 64);
+                if (cap > in_next) {
+                    const unsigned r = in_next + 1 + lane;
+                    const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
+                    const unsigned long long ok = __ballot(e1.x != HAND_SENT);
+                    const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;
+                    if (k > 0) {
+                        if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
+                        const unsigned hi = in_next + k;
+                        if (lane == 0) lds_st(prod(0), hi == (unsigned)m ? rows_end : hi);
+                        in_next = hi;
+                        moved = true;
+                    }
+                }
+            } else if (in_next < (unsigned)m) {
                 const unsigned space = lds_ld(cons(0)) + RING;
                 const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
@@ -984,13 +1021,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                         // H'(m, n): the cost (a partial last stripe's compute wave writes it)
                         if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
                     }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) {
-                        g_st(p.hand_prog + g, hi);
-                        if (p.edge_prog != nullptr && last_slab)
-                            __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
-                        lds_st(cons(nlive), hi);
+                    if (!out_sent) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) __hip_atomic_store(p.edge_prog, hi, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
                     }
+                    if (lane == 0) lds_st(cons(nlive), hi);
                     out_next = hi;
                     moved = true;
                 }
