@@ -481,15 +481,20 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // (its query-profile ring deeper than a workgroup's skew: NWC stripes x 64*TD steps)
     int qrows = c->qrows;
     c->diag = false;
-    // automatic: score-only fills of tall, narrow problems on one GPU (m >= 6 n, <= 8 stripes per CU:
-    // 1M x 125k fills in 95 ms against 107 ms for the row scan; the row scan wins on square shapes,
-    // where the anti-diagonal skew of 64 steps per stripe costs more, profiles/r01/diag_sweep.txt).
-    // Not for a slab of a multi-GPU fill: there the next rank starts when this one's last stripe
-    // does, and that start (the ramp) is 15 ms for the anti-diagonal fill against 3.6 ms.
-    const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && !c->slab && m >= 6 * n &&
-                           (n + 63) / 64 <= 8 * (int64_t)c->num_cu;
+    // automatic: score-only fills of tall problems on one GPU (m >= 4 n, <= 8 stripes per CU).
+    // Measured (profiles/r01/diag_sweep.txt): 1M x 125k 80 ms (TD = 1) against 107 ms for the row
+    // scan, 1M x 250k 126 ms (TD = 2) against 141 ms; the row scan wins on square shapes (C4 313 ms
+    // against 400 ms), where the anti-diagonal skew of 64 steps per stripe costs more.  Not for a
+    // slab of a multi-GPU fill: there the next rank starts when this one's last stripe does, and
+    // that start (the ramp) is ~15 ms for the anti-diagonal fill against ~3 ms for the row scan.
+    const int auto_td = (n + 63) / 64 <= 8 * (int64_t)c->num_cu ? 1 : 2;
+    const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && !c->slab && m >= 4 * n &&
+                           (n + 64 * auto_td - 1) / (64 * auto_td) <= 8 * (int64_t)c->num_cu;
     if ((!tb || (full && c->qbytes == 1)) && (c->diag_req == 2 || auto_diag) && bd.ckpt == nullptr) {
-        const int td = full ? std::min(std::max(c->diag_T_req, 1), 2) : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req : 1;
+        int td = full ? std::min(std::max(c->diag_T_req, 1), 2)
+                      : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req
+                      : auto_diag ? auto_td : 1;
+        if (c->qbytes == 2) td = std::min(td, 2);  // int16 profiles at TD = 4 spill
         set_stripes(c, td, false, false, n);
         if (full) {  // the debug FULL variant is built for 4 compute waves
             c->nwc = 4;

@@ -920,6 +920,34 @@ __device__ void fill_blocked(FillArgs& p, unsigned* cnt, int2* ring, QT* qring, 
 // so lane 63 always carries column n of the partial stripe: the right edge and the
 // cost come out of the same ring as for a full stripe.
 constexpr int QMIRROR = 16;
+constexpr int DSUB = 8;  // steps per sub-chunk of the anti-diagonal fill (edge read / wait / publish unit)
+
+// lane 63's publication of eight rows (carry + the sub-chunk's first seven): (H', h1') pairs with one
+// ds_write2_b32 each (no packing into consecutive registers), then {cons, prod}; exec narrowed as
+// in lds_publish
+__device__ __forceinline__ void lds_publish8(unsigned ring_addr, unsigned pc_addr, unsigned long long lanemask, int cH,
+                                             int cX, const int (&h)[DSUB], const int (&x)[DSUB], unsigned cons,
+                                             unsigned prod) {
+    unsigned long long saved;
+    const v2u cp = {cons, prod};
+    asm volatile(
+        "s_mov_b64 %0, exec\n\ts_mov_b64 exec, %3\n\t"
+        "ds_write2_b32 %1, %4, %5 offset0:0 offset1:1\n\t"
+        "ds_write2_b32 %1, %6, %7 offset0:2 offset1:3\n\t"
+        "ds_write2_b32 %1, %8, %9 offset0:4 offset1:5\n\t"
+        "ds_write2_b32 %1, %10, %11 offset0:6 offset1:7\n\t"
+        "ds_write2_b32 %1, %12, %13 offset0:8 offset1:9\n\t"
+        "ds_write2_b32 %1, %14, %15 offset0:10 offset1:11\n\t"
+        "ds_write2_b32 %1, %16, %17 offset0:12 offset1:13\n\t"
+        "ds_write2_b32 %1, %18, %19 offset0:14 offset1:15\n\t"
+        "ds_write_b64 %2, %20\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(ring_addr), "v"(pc_addr), "s"(lanemask), "v"(cH), "v"(cX), "v"(h[0]), "v"(x[0]), "v"(h[1]), "v"(x[1]),
+          "v"(h[2]), "v"(x[2]), "v"(h[3]), "v"(x[3]), "v"(h[4]), "v"(x[4]), "v"(h[5]), "v"(x[5]), "v"(h[6]),
+          "v"(x[6]), "v"(cp)
+        : "memory");
+}
 
 template <typename QT, int NWC, int TD, bool FULL, bool DBG>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
@@ -1102,10 +1130,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     // slot (r - 1) & RMASK of a ring holds (H', h1') of row r.  Edges are read one sub-chunk
     // (4 steps) ahead into ping-pong registers, the producer's counter one sub-chunk ahead of its
     // use, the profile one chunk ahead.
-    wait_ge(prod(w), 0, avail, 4, 0);
-    int4 A01 = reinterpret_cast<const int4*>(rin)[0];  // rows 1..4 (sub-chunk 0)
-    int4 A23 = reinterpret_cast<const int4*>(rin)[1];
-    int4 B01, B23;
+    wait_ge(prod(w), 0, avail, DSUB, 0);
+    int4 A[DSUB / 2], B[DSUB / 2];  // (H', h1') of two rows each: rows 1..8 (sub-chunk 0) in A
+#pragma unroll
+    for (int k = 0; k < DSUB / 2; k++) A[k] = reinterpret_cast<const int4*>(rin)[k];
     unsigned pnext = *prod_in;
     int cH = 0, cX = 0;  // lane 63's last column's (H', h1') of the last step of the previous sub-chunk
     // column k of this lane works on row t - (lane*TD + k) + 1 at step t: its 16 profile values of
@@ -1170,50 +1198,54 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
             subn[k].load_unaligned(qcol[k] + (((unsigned)(t0 + FROWS - (lane * TD + k))) & qmask));
         auto sub_chunks = [&](auto MASKED) {
 #pragma unroll
-            for (int sc = 0; sc < FROWS / 4; sc++) {
-                const int r0 = __builtin_amdgcn_readfirstlane(t0 + 4 * sc);  // steps r0 .. r0+3: lane 0 rows r0+1 .. r0+4
-                // this sub-chunk's edges (read a sub-chunk ago) and the next one's (FROWS / 4 is even)
-                const int4& C01 = (sc & 1) ? B01 : A01;
-                const int4& C23 = (sc & 1) ? B23 : A23;
-                int4& N01 = (sc & 1) ? A01 : B01;
-                int4& N23 = (sc & 1) ? A23 : B23;
-                const int eh[4] = {C01.x, C01.z, C23.x, C23.z};
-                const int ex[4] = {C01.y, C01.w, C23.y, C23.w};
-                // left edges one sub-chunk ahead: rows r0+5 .. r0+8 (slots r0+4 .. r0+7)
-                wait_ge(prod(w), 0, avail, r0 + 8, 0);
+            for (int sc = 0; sc < FROWS / DSUB; sc++) {
+                const int r0 = __builtin_amdgcn_readfirstlane(t0 + DSUB * sc);  // steps r0 .. r0+7: lane 0 rows r0+1 .. r0+8
+                // this sub-chunk's edges (read a sub-chunk ago) and the next one's (FROWS / DSUB is even)
+                int4(&C)[DSUB / 2] = (sc & 1) ? B : A;
+                int4(&N)[DSUB / 2] = (sc & 1) ? A : B;
+                int eh[DSUB], ex[DSUB];
+#pragma unroll
+                for (int k = 0; k < DSUB / 2; k++) {
+                    eh[2 * k] = C[k].x; ex[2 * k] = C[k].y; eh[2 * k + 1] = C[k].z; ex[2 * k + 1] = C[k].w;
+                }
+                // left edges one sub-chunk ahead: rows r0+9 .. r0+16 (slots r0+8 .. r0+15)
+                wait_ge(prod(w), 0, avail, r0 + 2 * DSUB, 0);
                 {
-                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + 4) & RMASK));
-                    N01 = e4[0];
-                    N23 = e4[1];
+                    const int4* e4 = reinterpret_cast<const int4*>(rin + ((r0 + DSUB) & RMASK));
+#pragma unroll
+                    for (int k = 0; k < DSUB / 2; k++) N[k] = e4[k];
                     pnext = *prod_in;
                 }
-                int oH[4], oX[4];
+                int oH[DSUB], oX[DSUB];
+                auto steps = [&](auto CAP) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    step(eh[u], ex[u], 4 * sc + u, r0 + u, MASKED);
-                    oH[u] = Hp[u & 1][TD - 1];
-                    oX[u] = Xo[TD - 1];
-                    if (tm == r0 + u) {  // uniform, once per stripe
+                    for (int u = 0; u < DSUB; u++) {
+                        step(eh[u], ex[u], DSUB * sc + u, r0 + u, MASKED);
+                        oH[u] = Hp[u & 1][TD - 1];
+                        oX[u] = Xo[TD - 1];
+                        if (decltype(CAP)::value && tm == r0 + u) {  // once per stripe
 #pragma unroll
-                        for (int k = 0; k < TD; k++)
-                            if (cn % TD == k) Hm = Hp[u & 1][k];
+                            for (int k = 0; k < TD; k++)
+                                if (cn % TD == k) Hm = Hp[u & 1][k];
+                        }
                     }
-                }
+                };
+                if ((unsigned)(tm - r0) < (unsigned)DSUB) steps(std::true_type{});
+                else steps(std::false_type{});
                 // the counter read before the block has landed: no wait on the LDS here, nor at the
                 // next sub-chunk's check (used after the publish, whose LDS operations the compiler
                 // does not count, it would wait for every LDS operation in flight)
                 asm volatile("" : "+v"(pnext));  // keeps the counter's use (and its wait) after the block
                 avail = sgpr_u(max(avail, pnext));
-                // lane 63's last column has rows r0-64TD+2 .. r0-64TD+5; it publishes the 4-slot-aligned
-                // group r0-64TD+1 .. r0-64TD+4 (the first from the previous sub-chunk) so a group never
+                // lane 63's last column has rows r0-64TD+2 .. r0-64TD+9; it publishes the 8-slot-aligned
+                // group r0-64TD+1 .. r0-64TD+8 (the first from the previous sub-chunk) so a group never
                 // straddles the ring's end; rows < 1 land in slots nobody reads before their real rows
                 // overwrite them
                 const int pr = r0 - 64 * TD + 1;
-                lds_publish(rout_lds + (unsigned)((pr - 1) & RMASK) * 8u, pc_lds, edgemask,
-                            v4i{cH, cX, oH[0], oX[0]}, v4i{oH[1], oX[1], oH[2], oX[2]}, (unsigned)(r0 + 4),
-                            (unsigned)max(pr + 3, 0));
-                cH = oH[3];
-                cX = oX[3];
+                lds_publish8(rout_lds + (unsigned)((pr - 1) & RMASK) * 8u, pc_lds, edgemask, cH, cX, oH, oX,
+                             (unsigned)(r0 + DSUB), (unsigned)max(pr + DSUB - 1, 0));
+                cH = oH[DSUB - 1];
+                cX = oX[DSUB - 1];
             }
         };
         if (FULL || t0 < 64 * TD) sub_chunks(std::true_type{});
@@ -1914,13 +1946,15 @@ static void launch_diag_one(hipStream_t s, const FillArgs& p) {
 
 template <int TD>
 static void launch_diag_td(hipStream_t s, const FillArgs& p, int qbytes) {
-    if (p.nwc == 4) {
-        if (qbytes == 1) launch_diag_one<int8_t, 4, TD, false>(s, p);
-        else launch_diag_one<int16_t, 4, TD, false>(s, p);
-    } else {
-        if (qbytes == 1) launch_diag_one<int8_t, 8, TD, false>(s, p);
-        else launch_diag_one<int16_t, 8, TD, false>(s, p);
+    if (qbytes == 2) {
+        if constexpr (TD <= 2) {  // the host caps int16 profiles at TD = 2 (TD = 4 spills)
+            if (p.nwc == 4) launch_diag_one<int16_t, 4, TD, false>(s, p);
+            else launch_diag_one<int16_t, 8, TD, false>(s, p);
+        }
+        return;
     }
+    if (p.nwc == 4) launch_diag_one<int8_t, 4, TD, false>(s, p);
+    else launch_diag_one<int8_t, 8, TD, false>(s, p);
 }
 
 void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full) {
