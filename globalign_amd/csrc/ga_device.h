@@ -28,7 +28,6 @@ struct FillArgs {
     const int2* left;         // [m+1] (H', h1') of the slab's left edge
     const unsigned* left_prog;  // rows of `left` available (nullptr: all)
     int2* hand;               // [nslabs][m+1] right edge of each workgroup slab
-    unsigned* hand_prog;      // [nslabs] rows published
     unsigned* ticket;         // slab ticket
     unsigned* abort_word;
     uint8_t* tb;              // traceback words or nullptr

@@ -514,14 +514,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // workgroup hand-off rows read by a successor start as ga::HAND_SENT (bytes 0x80)
     if (c->nslabs > 1)
         HIPCHK(hipMemsetAsync(c->hand.p, 0x80, sizeof(int2) * (size_t)(c->nslabs - 1) * (m + 1), c->stream));
-    HIPCHK(c->flags.ensure(sizeof(unsigned) * (c->nslabs + 16)));
+    HIPCHK(c->flags.ensure(sizeof(unsigned) * 16));
     if (full) {
         if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
         HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
     }
     unsigned* fl = c->flags.as<unsigned>();
-    // flags layout: [0] ticket, [1] abort, [16..16+nslabs) hand progress
-    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * (c->nslabs + 16), c->stream));
+    // flags layout: [0] ticket, [1] abort
+    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * 16, c->stream));
     if (!bd.band)
         ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global,
                             c->gh.as<int>(), c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(),
@@ -543,7 +543,6 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.left_prog = nullptr;
     }
     p.hand = c->hand.as<int2>();
-    p.hand_prog = fl + 16;
     p.ticket = fl;
     p.abort_word = fl + 1;
     p.tb = tb ? c->tb.as<uint8_t>() : nullptr;

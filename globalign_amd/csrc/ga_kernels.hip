@@ -411,9 +411,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
     if (w == NWC) {
         // ---------------- IO wave: slab edges HBM <-> LDS rings, query profile ----------------
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
-        const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
+        const unsigned* src_prog = g == 0 ? p.left_prog : nullptr;  // g > 0: the rows themselves (in_sent)
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
-        const bool src_sc1 = g != 0 || p.left_prog != nullptr;
+        const bool src_sc1 = p.left_prog != nullptr;  // another GPU's edge, landing while the fill runs
         const bool last_slab = g == p.nslabs - 1;
         int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
         int2* rin0 = ring;
@@ -977,9 +977,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
     if (w == NWC) {
         // ---------------- IO wave: slab edges HBM <-> LDS rings, query profile ----------------
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
-        const unsigned* src_prog = g == 0 ? p.left_prog : p.hand_prog + (g - 1);
+        const unsigned* src_prog = g == 0 ? p.left_prog : nullptr;  // g > 0: the rows themselves (in_sent)
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
-        const bool src_sc1 = g != 0 || p.left_prog != nullptr;
+        const bool src_sc1 = p.left_prog != nullptr;  // another GPU's edge, landing while the fill runs
         const bool last_slab = g == p.nslabs - 1;
         int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
         int2* rin0 = ring;
