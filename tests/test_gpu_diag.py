@@ -72,3 +72,24 @@ def test_diag_custom_boundary(monkeypatch, td):
     row0[:3] = col0[:3] = 0
     got, cmat, goc = _fill(monkeypatch, td, s1, s2, SCORING, row0=row0, col0=col0)
     assert got == _oracle_cost(s1, s2, cmat, goc, row0, col0)
+
+
+@pytest.mark.parametrize("m,n", [(20_000, 3_000), (9_000, 2_100 + 37)])
+def test_auto_tall_score_vs_oracle(monkeypatch, m, n):
+    """No override: a score-only fill with m >= 4n takes the anti-diagonal kernel by itself (TD = 1 up to
+    131k columns); its cost must equal the oracle's like every other fill's."""
+    from globalign_amd import _native
+    from globalign_amd._native import CostTables
+    from globalign_amd.scoring import validate_and_transform_args
+    monkeypatch.delenv("GA_FILL_MODE", raising=False)
+    monkeypatch.delenv("GA_DIAG_COLS_PER_LANE", raising=False)
+    s1, s2 = splitmix_seq(m, m + 3, "dna"), splitmix_seq(n, n + 5, "dna")
+    _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **SCORING)
+    tables = CostTables(cmat, goc)
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(s1), tables.codes(s2), tables)
+        got = int(eng.fill(traceback=False)[0])
+    finally:
+        eng.close()
+    assert got == _oracle_cost(s1, s2, cmat, goc)
