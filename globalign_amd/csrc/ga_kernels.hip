@@ -1218,6 +1218,31 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                 }
                 int oH[DSUB], oX[DSUB];
                 auto steps = [&](auto CAP) {
+                    if constexpr (TD == 1 && !decltype(MASKED)::value && !decltype(CAP)::value) {
+                        // one column per lane, no masks: two hand-scheduled 4-step blocks (ga_row.h
+                        // diag4_asm); the state moves in and out of the parity-buffered form
+                        constexpr int QB = (int)sizeof(QT);
+                        int H = Hp[1][0], X = Xo[0], Y = Yc[0];
+#pragma unroll
+                        for (int hb = 0; hb < DSUB / 4; hb++) {
+                            const int u0 = DSUB * sc + 4 * hb;
+                            int o4H[4], o4X[4];
+                            diag4_asm<QB == 2>(eh[4 * hb], eh[4 * hb + 1], eh[4 * hb + 2], eh[4 * hb + 3], ex[4 * hb],
+                                               ex[4 * hb + 1], ex[4 * hb + 2], ex[4 * hb + 3], Hd0, H, X, Y,
+                                               sub[0].w[(u0 * QB) >> 2], sub[0].w[((u0 + 2) * QB) >> 2], o, o4H, o4X);
+                            Hd0 = eh[4 * hb + 3];
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                oH[4 * hb + u] = o4H[u];
+                                oX[4 * hb + u] = o4X[u];
+                            }
+                        }
+                        Hp[0][0] = oH[DSUB - 2];
+                        Hp[1][0] = oH[DSUB - 1];
+                        Xo[0] = X;
+                        Yc[0] = Y;
+                        return;
+                    }
 #pragma unroll
                     for (int u = 0; u < DSUB; u++) {
                         step(eh[u], ex[u], DSUB * sc + u, r0 + u, MASKED);
