@@ -1,4 +1,5 @@
 set -o pipefail
+# (ran against a one-off build with a T = 6 / NWC = 12 instantiation, since removed: 354 ms vs 313 ms for T = 8 / NWC = 8)
 # C4 with 6 columns per lane and 12 compute waves per workgroup (3 waves per SIMD), experiment build
 mkdir -p gpurun_out
 export GA_LIB_PATH=$PWD/globalign_amd/_lib/var/lib_t6.so
