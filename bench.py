@@ -1,27 +1,33 @@
 #!/usr/bin/env python3
 """Benchmark: DP cells/s of globalign's hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c3|c5|c2] [--no-cpu-baseline]
-                    [--no-headline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4|c4tb|c5|c2|c1]
+                    [--no-cpu-baseline] [--no-extra]
 
 Workloads (BASELINE.json configs, SURVEY 8d SplitMix64 inputs, resident in HBM):
-  c4 (default): 1M x 1M DNA, match 2 / mismatch -3 / open -5 / ext -1, score only.  BASELINE's
-                1/2/4/8-GPU scaling config: the SAME pair for every N (strong scaling), cut into
-                N column slabs whose edges stream between GPUs in row bands over RCCL
-                (globalign_amd/distributed.py).  A step = boundary + fill + score.
-  c3:           100k x 100k DNA, same scoring, full traceback: a step is the whole
+  c3 (default at N=1): 100k x 100k DNA, match 2 / mismatch -3 / open -5 / ext -1, full traceback --
+                the config BASELINE's roofline target is quoted on.  A step is the whole
                 find_global_alignment DP (fill + tie-break table + walk + strings,
-                globaligner.py:258-302).  At N=1 the default run also measures this headline
-                config and reports it as "headline_c3".
-  c4tb:         C4 with full traceback on one GPU: 10^12 traceback bytes do not fit in HBM, so the
-                traceback runs in row bands (a checkpointing score pass, then band refills + walk).
+                globaligner.py:258-302).  The N=1 line also carries "c4": one GPU's point of
+                the C4 scaling curve.
+  c4 (default at N>1): 1M x 1M DNA, same scoring, score only.  BASELINE's 1/2/4/8-GPU scaling
+                config: the SAME pair for every N (strong scaling), cut into N column slabs whose
+                edges stream between GPUs in row bands over RCCL (globalign_amd/distributed.py).
+  c4tb:         C4 with full traceback on one GPU (banded: a checkpointing score pass, then band
+                refills + walk; 10^12 traceback bytes do not fit in HBM).
   c5:           20k x 20k protein (seeds 3, 4), BLOSUM62, gap_open_score -10, full traceback.
   c2:           10k x 10k DNA, full traceback.
+  c1:           1k x 1k DNA (BASELINE configs[0], the reference's CPU-runnable case).
+
+--gpus N > 1 without a torch.distributed launcher environment starts N rank processes itself
+(torch.distributed.run, 127.0.0.1) and exits with their status; it fails if fewer than N GPUs
+are visible (GA_DIST_BACKEND=gloo rehearses the ranks without that check).
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,22 +42,32 @@ BYTES_PER_CELL_TB = 26  # 24 B/cell fill (M, Ix, Iy int32 written + r
 BYTES_PER_CELL = 24
 SCORING = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
 PROTEIN_SCORING = dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)
+DNA_SCORING_DESC = "match 2 / mismatch -3 / open -5 / ext -1"
 
 WORKLOADS = {
+    "c1": dict(m=1_000, n=1_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING,
+               desc=f"C1: 1k x 1k DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, full traceback"),
     "c2": dict(m=10_000, n=10_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING,
-               desc="C2: 10k x 10k DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / ext -1, full traceback"),
+               desc=f"C2: 10k x 10k DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, full traceback"),
     "c3": dict(m=100_000, n=100_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING,
-               desc="C3: 100k x 100k DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / ext -1, "
-                    "full traceback"),
+               desc=f"C3: 100k x 100k DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, full traceback"),
     "c4": dict(m=1_000_000, n=1_000_000, traceback=False, alphabet="dna", seeds=(1, 2), scoring=SCORING,
-               desc="C4: 1M x 1M DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / ext -1, score only"),
+               desc=f"C4: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, score only"),
     "c4tb": dict(m=1_000_000, n=1_000_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING, golden="c4",
-                 desc="C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), match 2 / mismatch -3 / open -5 / "
-                      "ext -1; banded traceback (checkpointed score pass + band refills, DESIGN.md 5.5)"),
+                 desc=f"C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}; banded "
+                      "traceback (checkpointed score pass + band refills, DESIGN.md 5.5)"),
     "c5": dict(m=20_000, n=20_000, traceback=True, alphabet="protein", seeds=(3, 4), scoring=PROTEIN_SCORING,
                desc="C5: 20k x 20k protein (SplitMix64 seeds 3,4), BLOSUM62, gap_open_score -10, full traceback"),
 }
-DEFAULT_WORKLOAD = "c4"
+SINGLE_GPU_DEFAULT = "c3"
+MULTI_GPU_DEFAULT = "c4"
+
+# committed profiles the roofline block is built from: PMC bytes and VALU
+# instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
+TRAFFIC_FILES = {"c3": "traffic.json", "c4": "traffic_c4.json"}
+VALU_FILES = {"c3": "valu_c3.json", "c4": "valu_c4.json"}
+VALU_MIX_FILES = {"c3": "r02/valu_mix_c3.json", "c4": "r02/valu_mix_c4.json"}
+VALU_RATE_FILE = "r02/valu_rate.txt"
 
 
 def splitmix(length, seed, alphabet="dna"):
@@ -77,35 +93,77 @@ def problem_tables(seq_1, seq_2, scoring=None):
     return _native.CostTables(cmat, goc), smat
 
 
-def cpu_baseline(sample=5000, traceback=False):
-    """The reference-equivalent pure-Python loop (oracle/pyport.py), 1 core, on a bounded sample of the
-    workload's kind (DNA, same scoring; fill only for score-only workloads, fill + traceback otherwise)."""
+def workload_pair(wl):
+    return splitmix(wl["m"], wl["seeds"][0], wl["alphabet"]), splitmix(wl["n"], wl["seeds"][1], wl["alphabet"])
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+def host_cores():
+    """CPU threads this process may use (the box sets OMP_NUM_THREADS to its CPU share)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(share))) if share and share.isdigit() else avail
+
+
+def cpu_baseline(py_sample=3000, c_sample=40_000, par_sample=100_000):
+    """The reference's CPU path timed on this host (rank 0, N = 1), three legs (BASELINE.md plan):
+    (1) the reference-equivalent pure-Python loop (oracle/pyport.py: nested lists of tuples, one keyword
+        call per cell as globaligner.py:317-392), 1 core -- the reported `value`;
+    (2) the C restatement (oracle/ga_oracle.c, int64 cells), 1 core;
+    (3) the same C cells as a column-slab x row-band wavefront over every host thread."""
     import random
-    from oracle import pyport
-    s1, s2 = splitmix(sample, 1), splitmix(sample, 2)
+    from oracle import core, pyport
+    s1, s2 = splitmix(py_sample, 1), splitmix(py_sample, 2)
     tables, _ = problem_tables(s1, s2)
     C = {x: {y: int(tables.sub[tables.code[x] * tables.K + tables.code[y]]) for y in tables.keys} for x in tables.keys}
     random.seed(0)
     t0 = time.perf_counter()
     T = pyport.fill(s1, s2, C, tables.gap_open, tables.max_cost)
-    if traceback:
-        pyport.traceback(T, s1, s2, C, tables.gap_open)
-    dt = time.perf_counter() - t0
-    what = "fill + traceback" if traceback else "fill + score (dp_array_forward, min of the last cell)"
-    return {"value": sample * sample / dt, "unit": "cells/s", "cores": 1, "kind": "port",
-            "sample": f"{sample}x{sample} DNA (SplitMix64 seeds 1,2), {what}, pure-Python port of the "
-                      f"reference loop (oracle/pyport.py), {dt:.1f} s"}
+    pyport.traceback(T, s1, s2, C, tables.gap_open)
+    dt_py = time.perf_counter() - t0
+    del T
+
+    def c_leg(L, threads):
+        a_s, b_s = splitmix(L, 1), splitmix(L, 2)
+        tab = core.Tables(C)
+        a, b = tab.codes(a_s), tab.codes(b_s)
+        row0, col0 = core.boundary(tab, a, b, tables.gap_open, (tab.max_cost + 1) * L)
+        t = time.perf_counter()
+        if threads == 1:
+            last = core.fill_score(tab, a, b, tables.gap_open, row0, col0)
+        else:
+            last = core.fill_score_parallel(tab, a, b, tables.gap_open, row0, col0, threads)
+        return L * L / (time.perf_counter() - t), int(min(last))
+
+    cores = host_cores()
+    c1_rate, _ = c_leg(c_sample, 1)
+    cp_rate, cp_cost = c_leg(par_sample, cores)
+    return {"value": py_sample * py_sample / dt_py, "unit": "cells/s", "cores": 1, "kind": "port",
+            "sample": f"{py_sample}x{py_sample} DNA (SplitMix64 seeds 1,2), fill + traceback, pure-Python port of the "
+                      f"reference loop (oracle/pyport.py, keyword call per cell as globaligner.py:317-392), "
+                      f"{dt_py:.1f} s",
+            "host_nproc": os.cpu_count(), "host_threads_available": cores,
+            "c_scalar_1core": {"value": c1_rate, "unit": "cells/s", "cores": 1,
+                               "sample": f"{c_sample}x{c_sample} DNA fill + score, oracle/ga_oracle.c"},
+            "c_threads_all_cores": {"value": cp_rate, "unit": "cells/s", "cores": cores,
+                                    "sample": f"{par_sample}x{par_sample} DNA (= C3 cells) fill + score, "
+                                              f"oracle/ga_oracle.c column-slab wavefront on {cores} threads",
+                                    "cost": cp_cost}}
 
 
-def load_traffic(name="traffic.json"):
-    """Measured HBM bytes per fill launch from a committed PMC summary (profiles/), if present."""
+# ----------------------------------------------------------------------------- profiles / roofline
+def _profile(name, key=None):
     path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
+    if not name or not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get("fill_kernel_hbm_bytes_per_launch")
+        d = json.load(open(path))
     except Exception:
         return None
+    return d.get(key) if key else d
 
 
 def golden_cost(workload):
@@ -116,10 +174,40 @@ def golden_cost(workload):
     return json.load(open(path)).get("cost")
 
 
-def workload_pair(wl):
-    return splitmix(wl["m"], wl["seeds"][0], wl["alphabet"]), splitmix(wl["n"], wl["seeds"][1], wl["alphabet"])
+def roofline(workload, wl, fill_ms, kernel="fill_kernel"):
+    """What bounds the fill, from the committed profiles.
+
+    The row-scan fill keeps M/X/Y in registers and LDS: it moves ~1 B/cell (PMC FETCH+WRITE), not the
+    24-26 B/cell of SURVEY 8(d)'s streaming model, and is VALU-issue bound.  So the bound is the VALU
+    issue rate: SQ_INSTS_VALU per launch / kernel time (HIP events on the launch stream) against the
+    chip's issue peak for the kernel's own op mix (tools/valu_mix.py over the hot loop, each form
+    priced by the measured microbenchmark profiles/r02/valu_rate.txt).  The HBM model is kept as a
+    secondary block."""
+    cells = wl["m"] * wl["n"]
+    bpc = BYTES_PER_CELL_TB if wl["traceback"] else BYTES_PER_CELL
+    traffic = _profile(TRAFFIC_FILES.get(workload, ""), "fill_kernel_hbm_bytes_per_launch")
+    insts = _profile(VALU_FILES.get(workload, ""), "sq_insts_valu_per_launch")
+    mix = _profile(VALU_MIX_FILES.get(workload, ""))
+    secs = fill_ms * 1e-3
+    hbm_alg = bpc * cells / secs / 1e9
+    out = {"bound": "valu", "achieved": None, "peak": None, "unit": "wave64 VALU instructions/s", "frac": None,
+           "traffic": traffic, "kernel": kernel, "kernel_ms": fill_ms, "units_per_launch": f"{cells} cells (m*n)",
+           "hbm": {"bytes_per_cell_algorithmic": bpc, "achieved_GBps": hbm_alg, "peak_GBps": HBM_PEAK_GBS,
+                   "frac": hbm_alg / HBM_PEAK_GBS,
+                   "measured_GBps": traffic / secs / 1e9 if traffic else None,
+                   "measured_bytes_per_cell": traffic / cells if traffic else None}}
+    if insts and mix:
+        rate = insts / secs
+        peak = mix["peak_valu_insts_per_s"]
+        out.update(achieved=rate, peak=peak, frac=rate / peak, insts_per_launch=insts, insts_per_cell=insts / cells,
+                   peak_model=f"1024 SIMDs x 2.4 GHz / {mix['mean_simd_cycles_per_op']:.3f} SIMD cycles per op "
+                              f"(hot-loop mix, profiles/{VALU_MIX_FILES[workload]}; rates {VALU_RATE_FILE})",
+                   sources=f"profiles/{VALU_FILES[workload]} (rocprofv3 SQ_INSTS_VALU), "
+                           f"profiles/{TRAFFIC_FILES[workload]} (FETCH_SIZE x2 + WRITE_SIZE)")
+    return out
 
 
+# ----------------------------------------------------------------------------- single GPU
 def measure_single(wl, steps, warmup):
     """Time `steps` passes of the hot path over one resident pair on cuda:0."""
     import random
@@ -152,72 +240,36 @@ def measure_single(wl, steps, warmup):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     cost = result[0]
+    out = {}
     if wl["traceback"]:
-        _, (a, mid, b), status, _ = result
+        _, (a, mid, b), status, mt_after = result
         assert status == 0 and a.replace("-", "") == s1 and b.replace("-", "") == s2
+        out["aln"] = (a, mid, b)
+        out["mt_after"] = mt_after
     cells = wl["m"] * wl["n"]
-    f_avg = float(np.mean(fill_ms))
-    return dict(elapsed=elapsed, cost=int(cost), cells=cells, value=cells * steps / elapsed,
-                ms_per_step=elapsed * 1e3 / steps, fill_ms=f_avg, walk_ms=float(np.mean(walk_ms)),
-                rng_ms=float(np.mean(rng_ms)))
-
-
-# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per 4 cycles per SIMD at the
-# single rate of v_min_i32 / DPP / VOP3 (tools/micro/valu_rate.hip; adds and logic ops dual-issue at 2 per 4)
-VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
-
-
-def load_valu(name):
-    """Measured fill-kernel wave-instructions per launch from a committed SQ counter summary (profiles/)."""
-    path = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(path):
-        return None
-    try:
-        return json.load(open(path)).get("sq_insts_valu_per_launch")
-    except Exception:
-        return None
-
-
-def roofline(wl, fill_ms, traffic, valu_insts=None):
-    """The HBM roofline of SURVEY 8(d) (algorithmic bytes per cell) plus what actually bounds the kernel:
-    it moves ~1 B/cell or less (traffic, PMC) and is VALU-issue bound, so the VALU issue rate is reported
-    against the single-rate wave-instruction peak beside it."""
-    bpc = BYTES_PER_CELL_TB if wl["traceback"] else BYTES_PER_CELL
-    cells = wl["m"] * wl["n"]
-    achieved = bpc * cells / (fill_ms * 1e-3) / 1e9
-    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-           "traffic": traffic, "kernel": "fill_kernel", "bytes_per_cell": bpc,
-           "units_per_launch": f"{cells} cells (m*n)", "kernel_ms": fill_ms,
-           "measured_hbm_GBps": (traffic / (fill_ms * 1e-3) / 1e9) if traffic else None}
-    if valu_insts:
-        rate = valu_insts / (fill_ms * 1e-3)
-        out["valu"] = {"insts_per_launch": valu_insts, "insts_per_cell": valu_insts / cells,
-                       "issue_rate": rate, "peak_single_rate": VALU_PEAK_INSTS, "frac": rate / VALU_PEAK_INSTS,
-                       "unit": "wave64 instructions/s", "source": "SQ_INSTS_VALU (profiles/valu_<workload>.json)"}
+    out.update(elapsed=elapsed, cost=int(cost), cells=cells, value=cells * steps / elapsed,
+               ms_per_step=elapsed * 1e3 / steps, fill_ms=float(np.mean(fill_ms)), walk_ms=float(np.mean(walk_ms)),
+               rng_ms=float(np.mean(rng_ms)))
     return out
 
 
-TRAFFIC_FILES = {"c3": "traffic.json", "c4": "traffic_c4.json"}
-VALU_FILES = {"c3": "valu_c3.json", "c4": "valu_c4.json"}
+def traceback_pin(workload, r):
+    """Alignment-string and random-state digests vs the oracle's (tests/golden/<workload>_aln.json)."""
+    path = os.path.join(ROOT, "tests", "golden", f"{workload}_aln.json")
+    if "aln" not in r or not os.path.exists(path):
+        return None
+    import hashlib
+    g = json.load(open(path))
+    a, mid, b = r["aln"]
+    dig = hashlib.sha256("\n".join([a, mid, b]).encode()).hexdigest()[:16]
+    st = hashlib.sha256(",".join(str(int(w)) for w in r["mt_after"]).encode()).hexdigest()[:32]
+    return {"aln_len": len(mid), "aln_sha16": dig, "state_sha32": st,
+            "matches_oracle": dig == g["aln_sha16"] and len(mid) == g["aln_len"] and st == g["state_sha32"]}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-headline", action="store_true", help="skip the C3 headline measurement at N=1")
-    ap.add_argument("--cpu-sample", type=int, default=5000)
-    args = ap.parse_args()
-    wl = WORKLOADS[args.workload]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
-        from globalign_amd import distributed
-        return distributed.bench_main(args, wl, args.workload)
+def single_line(args, workload, wl):
     r = measure_single(wl, args.steps, args.warmup)
-    gold = golden_cost(wl.get("golden", args.workload))
+    gold = golden_cost(wl.get("golden", workload))
     line = {
         "metric": METRIC,
         "value": r["value"],
@@ -234,26 +286,76 @@ def main():
         "config": {"workload": wl["desc"], "m": wl["m"], "n": wl["n"], "traceback": wl["traceback"],
                    "parallelism": "single GPU", "cost": r["cost"], "oracle_cost": gold,
                    "cost_matches_oracle": (r["cost"] == gold) if gold is not None else None},
-        "roofline": roofline(wl, r["fill_ms"], load_traffic(TRAFFIC_FILES.get(args.workload, "none.json")),
-                             load_valu(VALU_FILES.get(args.workload, "none.json"))),
+        "roofline": roofline(workload, wl, r["fill_ms"]),
+        "fill_ms": r["fill_ms"],
         "fill_cells_per_s": r["cells"] / (r["fill_ms"] * 1e-3),
     }
     if wl["traceback"]:
         line["walk_ms"] = r["walk_ms"]
         line["host_tiebreak_ms"] = r["rng_ms"]
-    if args.workload == DEFAULT_WORKLOAD and not args.no_headline:
-        # the north-star 1-GPU config: 100k x 100k with full traceback (BASELINE configs[2])
-        w3 = WORKLOADS["c3"]
-        h = measure_single(w3, max(3, min(args.steps, 5)), 1)
-        line["headline_c3"] = {"workload": w3["desc"], "value": h["value"], "unit": "cells/s",
-                               "ms_per_step": h["ms_per_step"], "cost": h["cost"], "fill_ms": h["fill_ms"],
-                               "walk_ms": h["walk_ms"], "host_tiebreak_ms": h["rng_ms"],
-                               "roofline": roofline(w3, h["fill_ms"], load_traffic("traffic.json"),
-                                                    load_valu("valu_c3.json"))}
+        line["config"]["traceback_pin"] = traceback_pin(workload, r)
+    if workload == SINGLE_GPU_DEFAULT and not args.no_extra:
+        # one GPU's point of BASELINE's C4 scaling curve (the same pair bench.py --gpus N slabs)
+        w4 = WORKLOADS["c4"]
+        h = measure_single(w4, max(2, min(args.steps, 5)), 1)
+        g4 = golden_cost("c4")
+        line["c4"] = {"workload": w4["desc"], "value": h["value"], "unit": "cells/s", "n_gpus": 1,
+                      "ms_per_step": h["ms_per_step"], "cost": h["cost"], "cost_matches_oracle": h["cost"] == g4,
+                      "fill_ms": h["fill_ms"], "roofline": roofline("c4", w4, h["fill_ms"])}
     if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample, traceback=wl["traceback"])
-    print(json.dumps(line))
+        line["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(line), flush=True)
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """bench.py --gpus N run without a launcher: start the N ranks (one process per GPU) and wait."""
+    backend = os.environ.get("GA_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch
+        ndev = torch.cuda.device_count()  # does not initialise the GPU (ROCm image)
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {ndev}", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C4 point of the N=1 line")
+    args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
+        return 2
+    workload = args.workload or (SINGLE_GPU_DEFAULT if args.gpus == 1 else MULTI_GPU_DEFAULT)
+    wl = WORKLOADS[workload]
+    if world > 1:
+        from globalign_amd import distributed
+        return distributed.bench_main(args, wl, workload)
+    single_line(args, workload, wl)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -42,7 +42,8 @@ EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
-    "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_last_kernel_ms", "ga_last_timings",
+    "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_ctx_wait_stream", "ga_ctx_stream_priority",
+    "ga_last_kernel_ms", "ga_last_timings",
 ]
 
 
@@ -116,6 +117,8 @@ def load_library():
         L.ga_stream_write.argtypes = [vp, vp, C.c_uint32]
         L.ga_ctx_stream.argtypes = [vp]
         L.ga_ctx_stream.restype = vp
+        L.ga_ctx_wait_stream.argtypes = [vp, vp]
+        L.ga_ctx_stream_priority.argtypes = [vp, C.POINTER(C.c_int)]
         L.ga_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ga_last_timings.argtypes = [vp, C.POINTER(C.c_float)]
         _lib = L
@@ -300,6 +303,15 @@ class Engine:
 
     def stream(self):
         return self._L.ga_ctx_stream(self._h)
+
+    def wait_stream(self, stream):
+        """Order this context's stream after the work enqueued so far on `stream` (a hipStream_t handle)."""
+        _check(self._L.ga_ctx_wait_stream(self._h, C.c_void_p(stream)))
+
+    def stream_priority(self):
+        pr = C.c_int(0)
+        _check(self._L.ga_ctx_stream_priority(self._h, C.byref(pr)))
+        return pr.value
 
     def stream_wait_ge(self, stream, prog_ptr, value):
         _check(self._L.ga_stream_wait_ge(C.c_void_p(stream), C.c_void_p(prog_ptr), int(value)))

@@ -285,7 +285,9 @@ void state_after(const RngTable& R, int64_t D, uint32_t* out) {
 // ------------------------------------------------------------------ context
 struct ga_ctx {
     int device = 0;
+    int priority = 0;  // of `stream` (the greatest the device offers, see ga_ctx_create)
     hipStream_t stream = nullptr;
+    hipEvent_t ev_dep = nullptr;  // ga_ctx_wait_stream
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // problem
     bool loaded = false, custom = false, filled_tb = false;
@@ -872,9 +874,25 @@ int ga_ctx_create(int device, ga_ctx** out) {
         if (const char* e = getenv("GA_FILL_MODE")) c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : 0;
         if (const char* e = getenv("GA_DIAG_COLS_PER_LANE")) c->diag_T_req = atoi(e);
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // The fill runs on a stream of the greatest priority.  HIP keeps a separate pool of hardware
+    // queues per priority (GPU_MAX_HW_QUEUES = 4 per pool and process), so no normal-priority
+    // stream -- torch's, RCCL's -- is ever put behind a running fill in the same in-order queue;
+    // a slab fill that waits on its halo needs the RCCL kernel that delivers it to run beside it
+    // (DESIGN.md 7).  GA_STREAM_PRIORITY=normal restores a default-priority stream (experiments).
+    {
+        int lo = 0, hi = 0;
+        const char* pe = getenv("GA_STREAM_PRIORITY");
+        const bool normal = pe && !strcmp(pe, "normal");
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+        c->priority = normal ? 0 : hi;  // 0: the default priority (lo is the LEAST, another pool)
+        if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->priority) != hipSuccess) {
+            delete c;
+            return fail(GA_E_HIP, "hipStreamCreateWithPriority failed");
+        }
+    }
+    if (hipEventCreateWithFlags(&c->ev_dep, hipEventDisableTiming) != hipSuccess) {
         delete c;
-        return fail(GA_E_HIP, "hipStreamCreate failed");
+        return fail(GA_E_HIP, "hipEventCreate failed");
     }
     for (auto& e : c->ev) {
         if (hipEventCreate(&e) != hipSuccess) {
@@ -897,6 +915,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_dep) (void)hipEventDestroy(c->ev_dep);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1057,6 +1076,19 @@ int ga_stream_write(void* stream, uint32_t* prog, uint32_t value) {
 }
 
 void* ga_ctx_stream(ga_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ga_ctx_wait_stream(ga_ctx* c, void* stream) {
+    if (int r = check_ctx(c)) return r;
+    HIPCHK(hipEventRecord(c->ev_dep, (hipStream_t)stream));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_dep, 0));
+    return GA_OK;
+}
+
+int ga_ctx_stream_priority(ga_ctx* c, int* priority) {
+    if (!c || !priority) return fail(GA_E_ARG, "null argument");
+    *priority = c->priority;
+    return GA_OK;
+}
 
 int ga_last_kernel_ms(ga_ctx* c, float* fill_ms, float* walk_ms) {
     if (!c) return fail(GA_E_ARG, "null context");

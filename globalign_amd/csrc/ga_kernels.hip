@@ -63,6 +63,22 @@ __device__ __forceinline__ void g_st64(int2* p, int2 v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), x, RLX, AGENT);
 }
 __device__ __forceinline__ int2 unpack64(unsigned long long x) { return make_int2((int)(unsigned)x, (int)(x >> 32)); }
+// A multi-GPU slab's halo and progress words: the left edge lands while the fill
+// runs (written by an RCCL kernel into device memory, or by the host into pinned memory) and the
+// right edge is read by the host / an RCCL kernel once its progress word covers it.  Both sides
+// use system-scope accesses (written through / read past every GPU cache), and the data stores
+// complete (s_waitcnt vmcnt(0)) before the progress word is stored.
+__device__ __forceinline__ unsigned s_ld(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), RLX, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long s_ld64(const int2* p) {
+    return __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<int2*>(p)), RLX,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void s_st64(int2* p, int2 v) {
+    unsigned long long x = (unsigned long long)(unsigned)v.x | ((unsigned long long)(unsigned)v.y << 32);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), x, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Bounded spin: returns false (and raises the abort word) after `limit` sleeps.
 __device__ __forceinline__ bool spin_ok(unsigned& spins, unsigned limit, unsigned* abort_word) {
@@ -469,13 +485,13 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             } else if (in_next < (unsigned)m) {
                 // ring 0 slots are free below cons[0]
                 const unsigned space = lds_ld(&pc.cons(0)) + RING;
-                const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
+                const unsigned avail = src_prog ? min(s_ld(src_prog), (unsigned)m) : (unsigned)m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
                     const unsigned r = in_next + 1 + lane;
                     if (r <= hi) {
-                        const int2 e1 = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
-                        const int h0 = r == 1 ? h00 : (src_sc1 ? unpack64(g_ld64(src + r - 1)) : src[r - 1]).x;
+                        const int2 e1 = src_sc1 ? unpack64(s_ld64(src + r)) : src[r];
+                        const int h0 = r == 1 ? h00 : (src_sc1 ? unpack64(s_ld64(src + r - 1)) : src[r - 1]).x;
                         rin0[(r - 1) & RMASK] = make_int2(h0, e1.y - o);
                     }
                     // rows past m are padding (garbage nobody reads back)
@@ -492,7 +508,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
                     const unsigned r = out_next + 1 + lane;
                     if (r <= hi) {
                         const int H = rout[r & RMASK].x;
-                        g_st64(dst + r, make_int2(H, rout[(r - 1) & RMASK].y + o));
+                        const int2 e = make_int2(H, rout[(r - 1) & RMASK].y + o);
+                        if (out_sent) g_st64(dst + r, e);
+                        else s_st64(dst + r, e);  // another GPU's halo
                         if (T == 1 && last_slab && r == (unsigned)m) p.out_last[0] = H;  // H'(m, n): the cost
                     }
                     if (!out_sent) {
@@ -1027,11 +1045,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                 }
             } else if (in_next < (unsigned)m) {
                 const unsigned space = lds_ld(cons(0)) + RING;
-                const unsigned avail = src_prog ? min(g_ld(src_prog), (unsigned)m) : (unsigned)m;
+                const unsigned avail = src_prog ? min(s_ld(src_prog), (unsigned)m) : (unsigned)m;
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
                     const unsigned r = in_next + 1 + lane;
-                    if (r <= hi) rin0[(r - 1) & RMASK] = src_sc1 ? unpack64(g_ld64(src + r)) : src[r];
+                    if (r <= hi) rin0[(r - 1) & RMASK] = src_sc1 ? unpack64(s_ld64(src + r)) : src[r];
                     // rows past m are padding (garbage only rows past m read)
                     if (lane == 0) lds_st(prod(0), hi == (unsigned)m ? rows_end : hi);
                     in_next = hi;
@@ -1045,7 +1063,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                     const unsigned r = out_next + 1 + lane;
                     if (r <= hi) {
                         const int2 e = rout[(r - 1) & RMASK];
-                        g_st64(dst + r, e);
+                        if (out_sent) g_st64(dst + r, e);
+                        else s_st64(dst + r, e);  // another GPU's halo
                         // H'(m, n): the cost (a partial last stripe's compute wave writes it)
                         if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
                     }

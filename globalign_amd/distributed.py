@@ -76,6 +76,27 @@ class Links:
         self.ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
         self.device_tensors = backend != "gloo"
 
+    def warm_up(self, dist, torch, device):
+        """Create the pair communicators now (one tiny exchange each way on every pair group).
+
+        RCCL sets a communicator up on its first send/recv; doing that while a slab fill is
+        already running would put its allocations and set-up kernels beside a persistent kernel
+        waiting on the very exchange being set up.  Collective over all ranks."""
+        if not self.device_tensors:
+            return
+        buf = torch.zeros(2, dtype=torch.int32, device=device)
+        for k in range(self.world - 1):
+            if self.rank not in (k, k + 1):
+                continue
+            g = self.right if self.rank == k else self.left
+            peer = k + 1 if self.rank == k else k
+            for sender in (k, k + 1):
+                if self.rank == sender:
+                    dist.send(buf, dst=peer, group=g)
+                else:
+                    dist.recv(buf, src=peer, group=g)
+        torch.cuda.synchronize(device)
+
 
 def stream_edges(dist, links, engine, halo_in, halo_out, m, band, timeout_s=600.0, poll_s=20e-6):
     """Exchange this rank's slab edges with its neighbours while its fill runs."""
@@ -128,8 +149,39 @@ def stream_edges(dist, links, engine, halo_in, halo_out, m, band, timeout_s=600.
         th.join()
     if errors:
         raise errors[0]
-    for w in sends:
-        w.wait()
+    # the sends must have READ halo_out before the next fill rewrites it: gloo completes them in
+    # wait(); an NCCL work's wait() only orders streams, so poll its completion event
+    t0 = time.monotonic()
+    for k, w in enumerate(sends):
+        if links.device_tensors:
+            while not w.is_completed():
+                if time.monotonic() - t0 > timeout_s:
+                    raise TimeoutError(f"rank {rank}: send of band {k} never completed")
+                time.sleep(poll_s)
+        else:
+            w.wait()
+
+
+def _halos(engine, links, m, torch):
+    """The slab's halo buffers, kept on the engine across steps (one allocation per problem size).
+
+    Their contents need no reset: the fill reads halo_in only below its progress word, and the
+    host sends halo_out rows only below the fill's.  With RCCL they are device tensors; with gloo
+    pinned (or, for CPU engines, plain) host tensors."""
+    shape, dtype = engine.halo_shape(m), engine.halo_dtype()
+    key = (shape, str(dtype), links.device_tensors)
+    cached = getattr(engine, "_halo_cache", None)
+    if cached is not None and cached[0] == key:
+        return cached[1], cached[2]
+    if links.device_tensors:
+        halo_in = torch.empty(shape, dtype=dtype, device=engine.torch_device())
+        halo_out = torch.empty(shape, dtype=dtype, device=engine.torch_device())
+    else:
+        pin = engine.pinned_halos()
+        halo_in = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+        halo_out = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+    engine._halo_cache = (key, halo_in, halo_out)
+    return halo_in, halo_out
 
 
 def _send_obj(dist, obj, dst, group):
@@ -154,16 +206,13 @@ def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_
     edges = slab_bounds(n, world)
     c0, c1 = edges[rank], edges[rank + 1]
     engine.load_slab(a_codes, b_codes, tables, c0, c1)
-    shape, dtype = engine.halo_shape(m), engine.halo_dtype()
-    if links.device_tensors:
-        halo_in = torch.zeros(shape, dtype=dtype, device=engine.torch_device())
-        halo_out = torch.zeros(shape, dtype=dtype, device=engine.torch_device())
-    else:
-        pin = engine.pinned_halos()
-        halo_in = torch.zeros(shape, dtype=dtype, pin_memory=pin)
-        halo_out = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+    halo_in, halo_out = _halos(engine, links, m, torch)
     engine.slab_bind_halos(halo_in.data_ptr() if rank > 0 else 0, halo_out.data_ptr() if rank < world - 1 else 0,
                            halo_in, halo_out)
+    if links.device_tensors:
+        # the halo tensors come from torch's allocator on torch's stream: the fill's stream
+        # starts after whatever that stream still has in flight
+        engine.order_after(torch.cuda.current_stream().cuda_stream)
     engine.slab_launch(traceback=traceback)
     if traceback:
         engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
@@ -241,6 +290,9 @@ class GpuSlabEngine:
     def slab_bind_halos(self, in_ptr, out_ptr, halo_in=None, halo_out=None):
         self.eng.slab_bind_halos(in_ptr, out_ptr)
 
+    def order_after(self, stream):
+        self.eng.wait_stream(stream)
+
     def slab_launch(self, traceback=True):
         self.eng.slab_launch(traceback)
 
@@ -265,6 +317,10 @@ class GpuSlabEngine:
     def timings(self):
         return self.eng.timings()
 
+    def synchronize(self):
+        import torch
+        torch.cuda.synchronize(self.device)
+
 
 def init_process_group():
     """torch.distributed from the torchrun environment (127.0.0.1 rendezvous)."""
@@ -283,43 +339,65 @@ def init_process_group():
     return dist, rank, world, local
 
 
+def _bench_engine(tables, local):
+    """The product engine on this rank's GPU, or (GA_BENCH_ENGINE=module:factory, CPU rehearsals
+    of the launcher in tests/) an engine the factory builds from the cost tables."""
+    spec = os.environ.get("GA_BENCH_ENGINE")
+    if spec:
+        import importlib
+        mod, fn = spec.split(":")
+        return getattr(importlib.import_module(mod), fn)(tables)
+    import torch
+    return GpuSlabEngine(local % max(1, torch.cuda.device_count()))  # ranks may share a GPU (gloo rehearsal)
+
+
 def bench_main(args, wl, workload):
     """bench.py --gpus N (N > 1): strong scaling of a workload over N GPUs.
 
     The SAME pair as the 1-GPU run (BASELINE C4 is the 1/2/4/8-GPU curve) is cut into N column
     slabs; a step is the distributed fill (+ traceback for traceback workloads) of that pair."""
+    import random
+
     import torch
+
     import bench
     dist, rank, world, local = init_process_group()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus}: torch.distributed reports {world} ranks")
     links = Links(dist, rank, world)
     m, n = wl["m"], wl["n"]
     s1, s2 = bench.workload_pair(wl)
     tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
     a_codes, b_codes = tables.codes(s1), tables.codes(s2)
-    import random
     random.seed(0)
     mt0 = np.array(random.getstate()[1], dtype=np.uint32)
-    engine = GpuSlabEngine(local % max(1, torch.cuda.device_count()))  # ranks may share a GPU (gloo rehearsal)
+    engine = _bench_engine(tables, local)
+    if links.device_tensors:
+        links.warm_up(dist, torch, engine.torch_device())
     result = None
     band = 4096 if m <= 200_000 else 8192
+    fill_ms = []
 
     def step():
-        return align_slabs(dist, links, engine, s1, s2, a_codes, b_codes, tables, mt0, band=band, torch=torch,
-                           traceback=wl["traceback"])
+        r = align_slabs(dist, links, engine, s1, s2, a_codes, b_codes, tables, mt0, band=band, torch=torch,
+                        traceback=wl["traceback"])
+        fill_ms.append(engine.timings()["fill_ms"])
+        return r
 
     for _ in range(args.warmup):
         result = step()
+    fill_ms.clear()
     dist.barrier()
-    torch.cuda.synchronize()
+    engine.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         result = step()
-    torch.cuda.synchronize()
+    engine.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX, group=links.ctrl)
-    elapsed = float(el.item())
+    stats = torch.tensor([elapsed, float(np.mean(fill_ms)) if fill_ms else 0.0], dtype=torch.float64)
+    dist.all_reduce(stats, op=dist.ReduceOp.MAX, group=links.ctrl)
+    elapsed, fill_max = float(stats[0]), float(stats[1])
     if rank == 0:
         cost = result[0]
         if wl["traceback"]:
@@ -327,6 +405,7 @@ def bench_main(args, wl, workload):
             assert status == 0 and sa.replace("-", "") == s1 and sb.replace("-", "") == s2
         gold = bench.golden_cost(workload)
         cells = m * n
+        edges = slab_bounds(n, world)
         line = {
             "metric": bench.METRIC,
             "value": cells * args.steps / elapsed,
@@ -343,12 +422,19 @@ def bench_main(args, wl, workload):
             "config": {"workload": f"{wl['desc']}; {world} column slabs, banded RCCL edge exchange ({band}-row bands)"
                                    + ("; right-to-left walk hand-off" if wl["traceback"] else ""),
                        "m": m, "n": n, "traceback": wl["traceback"], "parallelism": f"column slabs x{world}",
-                       "cost": int(cost), "oracle_cost": gold,
+                       "backend": dist.get_backend(), "cost": int(cost), "oracle_cost": gold,
                        "cost_matches_oracle": (int(cost) == gold) if gold is not None else None},
+            # every rank's slab fill is one persistent launch; its time (HIP events, max over ranks)
+            # includes the pipeline wait for the left neighbour's first band
+            "slab_fill_ms_max": fill_max,
+            "slab_columns": [b - a for a, b in zip(edges, edges[1:])],
+            "roofline": bench.roofline(f"{workload}_slab{world}", dict(wl, n=max(b - a for a, b in zip(edges, edges[1:]))),
+                                       fill_max) if fill_max > 0 else None,
         }
         print(json.dumps(line), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    return 0
 
 
 import json  # noqa: E402  (used by bench_main)

@@ -135,8 +135,17 @@ int ga_slab_mt_state(ga_ctx* ctx, int64_t D, uint32_t* mt_state_out);
 /* Enqueue on `stream` (a hipStream_t): wait until *prog >= value / write value to *prog. */
 int ga_stream_wait_ge(void* stream, uint32_t* prog, uint32_t value);
 int ga_stream_write(void* stream, uint32_t* prog, uint32_t value);
-/* The context's compute stream (hipStream_t). */
+/* The context's compute stream (hipStream_t).  It is created with the
+ * device's greatest stream priority, so it owns a hardware queue that no
+ * normal-priority stream (torch's, RCCL's) shares: a slab fill waiting on its
+ * halo never holds up the RCCL kernel that delivers it. */
 void* ga_ctx_stream(ga_ctx* ctx);
+/* Order the context's stream after all work enqueued so far on `stream`
+ * (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream): buffers that
+ * stream allocated or initialised are then safe for the next fill. */
+int ga_ctx_wait_stream(ga_ctx* ctx, void* stream);
+/* The priority the context's stream was created with (hipDeviceGetStreamPriorityRange units). */
+int ga_ctx_stream_priority(ga_ctx* ctx, int* priority);
 
 /* ---- measurement --------------------------------------------------------- */
 /* Device time (ms, HIP events on the launch stream) of the last fill kernel

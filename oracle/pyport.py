@@ -11,15 +11,22 @@ representative of running the reference itself on the same host
 import random
 
 
-def _cell(T, i, j, a, b, C, o):
-    d, l, u = T[i - 1][j - 1], T[i][j - 1], T[i - 1][j]
-    x, y = a[i - 1], b[j - 1]
-    return (min((d[0], d[1], d[2])) + C[x][y],
-            min((l[0] + o, l[1], l[2] + o)) + C["-"][y],
-            min((u[0] + o, u[1] + o, u[2])) + C[x]["-"])
+def next_costs(dp_array, i, j, seq_1, seq_2, costing_mat, gap_open_cost):
+    """One cell, in the call shape of the reference's get_next_best_costs (globaligner.py:317-363):
+    keyword arguments, nine nested-list reads of the three neighbours, three tuples, three min()."""
+    a_idx, b_idx = i - 1, j - 1
+    via_diag = (dp_array[i - 1][j - 1][0], dp_array[i - 1][j - 1][1], dp_array[i - 1][j - 1][2])
+    via_left = (dp_array[i][j - 1][0] + gap_open_cost, dp_array[i][j - 1][1],
+                dp_array[i][j - 1][2] + gap_open_cost)
+    via_up = (dp_array[i - 1][j][0] + gap_open_cost, dp_array[i - 1][j][1] + gap_open_cost,
+              dp_array[i - 1][j][2])
+    return (min(via_diag) + costing_mat[seq_1[a_idx]][seq_2[b_idx]],
+            min(via_left) + costing_mat["-"][seq_2[b_idx]],
+            min(via_up) + costing_mat[seq_1[a_idx]]["-"])
 
 
 def fill(a, b, C, o, max_cost):
+    """make_dp_array (:756-821) + dp_array_forward (:366-392): one keyword call per cell."""
     m, n = len(a), len(b)
     T = [[None] * (n + 1) for _ in range(m + 1)]
     big = (max_cost + 1) * max(m, n)
@@ -34,7 +41,7 @@ def fill(a, b, C, o, max_cost):
         T[i][0] = (big, big, acc)
     for i in range(1, m + 1):
         for j in range(1, n + 1):
-            T[i][j] = _cell(T, i, j, a, b, C, o)
+            T[i][j] = next_costs(dp_array=T, i=i, j=j, seq_1=a, seq_2=b, costing_mat=C, gap_open_cost=o)
     return T
 
 

@@ -6,6 +6,8 @@
 #include <algorithm>
 
 #define OPS4(op) ".rept 64\n" op " %0, %0, %4\n" op " %1, %1, %4\n" op " %2, %2, %4\n" op " %3, %3, %4\n.endr\n"
+#define OPS4_S(op, suf) ".rept 64\n" op " %0, %4, %0 " suf "\n" op " %1, %4, %1 " suf "\n" op " %2, %4, %2 " suf "\n" op " %3, %4, %3 " suf "\n.endr\n"
+#define OPS4_M(op, suf) ".rept 64\n" op " %0, %4 " suf "\n" op " %1, %4 " suf "\n" op " %2, %4 " suf "\n" op " %3, %4 " suf "\n.endr\n"
 #define OPS4_3(op) ".rept 64\n" op " %0, %0, %4, %1\n" op " %1, %1, %4, %2\n" op " %2, %2, %4, %3\n" op " %3, %3, %4, %0\n.endr\n"
 
 template <int V>
@@ -39,6 +41,13 @@ __global__ void indep(long long* out, int* sink) {
         if (V == 21) R(OPS4_3("v_add_lshl_u32"));
         if (V == 22) R(OPS4("v_pk_max_i16"));
         if (V == 23) R(OPS4_3("v_min3_u32"));
+        // forms the fill's hot loop uses (tools/valu_mix.py); the DPP / SDWA source is the
+        // loop-invariant %4, so no VALU->DPP hazard applies
+        if (V == 24) R(OPS4_S("v_min_i32_dpp", "row_shr:1 row_mask:0xf bank_mask:0xf"));
+        if (V == 25) R(OPS4_M("v_mov_b32_dpp", "row_shr:1 row_mask:0xf bank_mask:0xf"));
+        if (V == 26) R(OPS4_M("v_mov_b32", ""));
+        if (V == 27) R(OPS4_S("v_add_u32_sdwa", "dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"));
+        if (V == 28) R(OPS4_S("v_min_i32_dpp", "row_bcast:15 row_mask:0xa bank_mask:0xf"));
 #undef R
     }
     long long t1 = __builtin_amdgcn_s_memtime();
@@ -66,11 +75,12 @@ int main() {
     const char* names[] = {"v_min_i32", "v_min_u32", "v_sub_u32", "v_max_i32", "v_med3_i32", "v_lshl_or_b32",
                            "v_or3_b32", "v_pk_min_i16", "v_pk_add_u16", "v_cvt_pk_u16_u32", "v_perm_b32", "v_add3_u32",
                            "v_bfe_i32", "v_and_b32", "v_or_b32", "v_lshlrev_b32", "v_min3_i32", "v_pk_min_u16",
-                           "v_min_i16", "v_sub_i32", "v_add_co_u32", "v_add_lshl_u32", "v_pk_max_i16", "v_min3_u32"};
+                           "v_min_i16", "v_sub_i32", "v_add_co_u32", "v_add_lshl_u32", "v_pk_max_i16", "v_min3_u32", "v_min_i32_dpp", "v_mov_b32_dpp", "v_mov_b32",
+                           "v_add_u32_sdwa", "v_min_i32_dpp bcast15"};
     auto fns = std::vector<void (*)(long long*, int*)>{
         indep<0>, indep<1>, indep<2>, indep<3>, indep<4>, indep<5>, indep<6>, indep<7>, indep<8>, indep<9>, indep<10>,
         indep<11>, indep<12>, indep<13>, indep<14>, indep<15>, indep<16>, indep<17>, indep<18>, indep<19>, indep<20>,
-        indep<21>, indep<22>, indep<23>};
+        indep<21>, indep<22>, indep<23>, indep<24>, indep<25>, indep<26>, indep<27>, indep<28>};
     const double n = 16.0 * 64 * 4;
     for (int v = 0; v < (int)fns.size(); v++) {
         double c1 = run(fns[v], 4, 256) / n, c2 = run(fns[v], 8, 256) / n;
