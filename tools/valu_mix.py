@@ -24,12 +24,16 @@ MEASURED = {
     "v_pk_min_i16": 4.24, "v_pk_add_u16": 4.24, "v_cvt_pk_u16_u32": 4.24, "v_perm_b32": 4.24,
     "v_add3_u32": 4.24, "v_bfe_i32": 4.24, "v_bfe_u32": 4.24, "v_min3_i32": 4.24, "v_min3_u32": 4.24,
     "v_pk_min_u16": 4.24, "v_add_lshl_u32": 4.24, "v_pk_max_i16": 4.24,
+    # DPP / SDWA forms are priced as themselves (the _dpp / _sdwa suffix is kept)
+    "v_min_i32_dpp": 4.24, "v_mov_b32_dpp": 4.24, "v_mov_b32": 2.02, "v_add_u32_sdwa": 4.24,
 }
 
 
 def cost(op):
     base = op[:-4] if op.endswith("_e32") or op.endswith("_e64") else op
-    base = base[:-4] if base.endswith("_dpp") else base
+    if base in MEASURED:
+        return MEASURED[base], True
+    base = base[:-4] if base.endswith("_dpp") else base[:-5] if base.endswith("_sdwa") else base
     if base in MEASURED:
         return MEASURED[base], True
     return 4.02, False  # unmeasured forms priced as the common half-rate v_min_i32
