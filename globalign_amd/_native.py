@@ -39,7 +39,7 @@ class EngineError(RuntimeError):
 
 # every symbol include/globalign_amd.h declares (tests check the exports)
 EXPORTS = [
-    "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill",
+    "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
     "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_ctx_wait_stream", "ga_ctx_stream_priority",
@@ -100,6 +100,7 @@ def load_library():
         L.ga_ctx_destroy.restype = None
         L.ga_problem_set.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), p32, p32]
         L.ga_problem_fill.argtypes = [vp, i32, pi64, p32]
+        L.ga_problem_set_cells.argtypes = [vp, p32, pi64]
         L.ga_problem_traceback.argtypes = [vp, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i64,
                                            pi64, p32]
         L.ga_problem_align.argtypes = [vp, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i64,
@@ -212,6 +213,15 @@ class Engine:
             ptr = out.ctypes.data_as(C.POINTER(C.c_int32))
         _check(self._L.ga_problem_fill(self._h, flags, C.byref(cost), ptr))
         return cost.value, out
+
+    def set_cells(self, cells):
+        """Use a filled (m+1, n+1, 3) int32 cell array for the next traceback (-> min of the last cell)."""
+        arr = np.ascontiguousarray(cells, dtype=np.int32)
+        if arr.shape != (self.m + 1, self.n + 1, 3):
+            raise ValueError(f"cells must be ({self.m + 1}, {self.n + 1}, 3), got {arr.shape}")
+        cost = C.c_int64(0)
+        _check(self._L.ga_problem_set_cells(self._h, arr.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(cost)))
+        return cost.value
 
     def _tb_call(self, fn, mt_words, a_chr, b_chr, extra=()):
         mt = np.ascontiguousarray(mt_words, dtype=np.uint32).copy()

@@ -74,6 +74,8 @@ int boundary_scratch_ints(int m, int n);  // ints of scratch launch_boundary nee
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows, int tb_stage_bytes_per_wave = 0);
 void launch_walk(hipStream_t s, const WalkArgs& w);
+// traceback words of a caller-supplied (m+1) x (n+1) x 3 cell array (dp_array_backward shim)
+void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)
 void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full);
 size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows);

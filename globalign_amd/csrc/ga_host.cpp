@@ -935,6 +935,26 @@ int ga_problem_fill(ga_ctx* c, int32_t flags, int64_t* cost_out, int32_t* full_o
     return finish_fill(c, cost_out, (flags & GA_FILL_FULL) ? full_out : nullptr);
 }
 
+int ga_problem_set_cells(ga_ctx* c, const int32_t* cells, int64_t* cost_out) {
+    if (int r = check_ctx(c)) return r;
+    if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
+    if (c->slab) return fail(GA_E_STATE, "slab contexts fill their own cells");
+    if (!cells || !cost_out) return fail(GA_E_ARG, "null argument");
+    const int64_t m = c->m, n = c->n;
+    if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "ga_problem_set_cells is for small problems");
+    c->TC = (int)((m + ga::FROWS - 1) / ga::FROWS) * c->CB;
+    HIPCHK(c->tb.ensure((size_t)((n + 63) / 64) * c->TC * 1024));
+    HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
+    HIPCHK(hipMemcpyAsync(c->full.p, cells, sizeof(int) * 3 * (m + 1) * (n + 1), hipMemcpyHostToDevice, c->stream));
+    ga::launch_tb_from_cells(c->stream, c->full.as<int>(), (int)m, (int)n, c->o, c->CB, c->TC, c->tb.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int32_t* last = cells + 3 * (m * (n + 1) + n);
+    *cost_out = std::min(std::min(last[0], last[1]), last[2]);  // min(dp_array[m][n]) (globaligner.py:425)
+    c->filled_tb = true;
+    return GA_OK;
+}
+
 int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
                          char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status) {
     if (int r = check_ctx(c)) return r;

@@ -1387,6 +1387,25 @@ __device__ __forceinline__ unsigned tb_code(const uint8_t* tb, int CB, int TC, i
     return v;
 }
 
+// dp_array_backward over a caller-supplied dp_array (the reference walks the CALLER's cells,
+// globaligner.py:425-514, whatever filled them): the traceback word of every interior cell from its
+// given (M, X, Y), in the fill's layout (tb_code above).  The word only needs the differences to
+// the cell's minimum, so any int32 triple is encoded exactly (saturated at o + 1 as the fill does).
+__global__ void __launch_bounds__(256) tb_from_cells_kernel(const int* __restrict__ cells, int m, int n, int o, int CB,
+                                                            int TC, uint8_t* __restrict__ tb) {
+    const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (k >= (long long)m * n) return;
+    const int i = (int)(k / n) + 1, j = (int)(k % n) + 1;
+    const int* v = cells + 3 * ((long long)i * (n + 1) + j);
+    const long long M = v[0], X = v[1], Y = v[2];
+    const long long H = min(min(M, X), Y), op1 = (long long)o + 1;
+    const int W = (8 * CB - 1) / 2;
+    const unsigned code = (unsigned)min(X - H, op1) | ((unsigned)min(Y - H, op1) << W) | ((M != H ? 1u : 0u) << (2 * W));
+    const int s = (j - 1) >> 6, l = (j - 1) & 63, t = i - 1, spc = 16 / CB;
+    uint8_t* p = tb + (((long long)s * TC + t / spc) * 64 + l) * 16 + (t % spc) * CB;
+    for (int q = 0; q < CB; q++) p[q] = (uint8_t)(code >> (8 * q));
+}
+
 constexpr int TT = 64;       // tile edge
 constexpr int TB4 = 4;       // tile block edge (tiles cached per axis)
 constexpr int TP = TB4 * TT; // torus pitch (256)
@@ -2010,6 +2029,12 @@ void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full) {
     if (p.cols_per_lane == 4) launch_diag_td<4>(s, p, qbytes);
     else if (p.cols_per_lane == 2) launch_diag_td<2>(s, p, qbytes);
     else launch_diag_td<1>(s, p, qbytes);
+}
+
+void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb) {
+    const long long cells_in = (long long)m * n;
+    hipLaunchKernelGGL(tb_from_cells_kernel, dim3((unsigned)((cells_in + 255) / 256)), dim3(256), 0, s, cells, m, n, o,
+                       CB, TC, tb);
 }
 
 void launch_walk(hipStream_t s, const WalkArgs& w) {

@@ -35,7 +35,9 @@ def _mt_words():
 
 
 def _set_mt_words(words):
-    random.setstate((3, tuple(int(x) for x in words), None))
+    # only the MT words move: random.choice leaves gauss_next (the state's third item) alone
+    st = random.getstate()
+    random.setstate((st[0], tuple(int(x) for x in words), st[2]))
 
 
 class GlobalAligner:
@@ -154,32 +156,55 @@ def dp_array_forward(dp_array, seq_1, seq_2, costing_mat, gap_open_cost):
 def dp_array_backward(dp_array, seq_1, seq_2, costing_mat, gap_open_cost):
     """Traceback of a filled dp_array -> (seq_1_aligned, middle_part, seq_2_aligned, cost) (globaligner.py:395-593).
 
-    The walk needs per-cell rank information, so the fill is recomputed on the
-    device from dp_array's row 0 / column 0."""
+    Like the reference it walks the CALLER's cells (edited or hand-made ones included): the whole
+    array goes to the device, a kernel derives every cell's traceback word from its (M, X, Y), and
+    the walk kernel follows them.  Every interior cell must hold a triple (the reference would
+    raise TypeError on a None it walks into; here any None raises it)."""
     m, n = len(seq_1), len(seq_2)
     tables = _native.CostTables(costing_mat, gap_open_cost)
-    row0, col0 = _boundary_arrays(dp_array, m, n)
+    try:
+        cells = np.array([[tuple(c) for c in row] for row in dp_array], dtype=np.int64)
+    except TypeError:
+        raise TypeError("'NoneType' object is not subscriptable") from None
+    if cells.shape != (m + 1, n + 1, 3):
+        raise IndexError("list index out of range")
+    if np.abs(cells).max(initial=0) >= 2 ** 31:
+        raise OverflowError("dp_array values exceed the int32 range of the device path")
+    cells = cells.astype(np.int32)
+    row0, col0 = cells[0].reshape(-1).copy(), cells[:, 0].reshape(-1).copy()
     eng = _native.default_engine()
     eng.load(tables.codes(seq_1), tables.codes(seq_2), tables, row0=row0, col0=col0)
-    cost, (a, mid, b), status, mt = eng.align(_mt_words(), seq_1, seq_2)
+    cost = eng.set_cells(cells)
+    (a, mid, b), status, mt = eng.traceback(_mt_words(), seq_1, seq_2)
     _set_mt_words(mt)
     if status == _native.GA_TB_INDEX_ERROR:
         raise IndexError("string index out of range")
     return a, mid, b, cost
 
 
+def _cli_version():
+    """version('globalign') as the reference's --version prints it (globaligner.py:31-36): the installed
+    globalign distribution's version, this package's own when globalign itself is not installed."""
+    from importlib.metadata import PackageNotFoundError, version
+    try:
+        return version("globalign")
+    except PackageNotFoundError:
+        return __version__
+
+
 def main(argv=None):
     """The `globaligner` command line (globaligner.py:23-129)."""
     parser = argparse.ArgumentParser(description="Perform optimal global alignment of two nucleotide or amino acid "
                                                  "sequences.")
-    parser.add_argument("--version", action="version", version=__version__, help="Prints the version and exits.")
+    parser.add_argument("--version", action="version", version=_cli_version(), help="Prints the version and exits.")
     parser.add_argument("-i", "--input_fasta", required=False,
                         help="FASTA file with the two sequences to align (only the first 2 records are used).")
     parser.add_argument("-o", "--output", required=False,
                         help="Output file for the alignment; stdout when omitted.")
     parser.add_argument("--seq_1", required=False, help="First sequence to align.")
     parser.add_argument("--seq_2", required=False, help="Second sequence to align.")
-    parser.add_argument("--scoring_mat_name", required=False, help="BLOSUM50 or BLOSUM62.")
+    parser.add_argument("--scoring_mat_name", required=False, choices=["BLOSUM50", "BLOSUM62"],
+                        help="Either 'BLOSUM50' or 'BLOSUM62'.")
     parser.add_argument("--scoring_mat_path", required=False, help="Path to a custom scoring matrix file.")
     parser.add_argument("--match_score", required=False, help="Score for a match (default 2).")
     parser.add_argument("--mismatch_score", required=False, help="Score for a mismatch (default -3).")

@@ -249,10 +249,12 @@ def read_seq_from_fasta(fasta_path):
 
 
 def read_first_2_seqs_from_fasta(fasta_path):
+    """The first two records (start.py:666-688).  Like the reference, a THIRD record is pulled from the
+    reader before stopping, so a malformed (empty) third record still raises."""
     seqs = []
     for _, seq in read_seq_from_fasta(fasta_path):
         seqs.append(seq)
-        if len(seqs) == 2:
+        if len(seqs) == 3:
             break
     if len(seqs) < 2:
         raise RuntimeError("Two sequences could not be read from the FASTA file.")

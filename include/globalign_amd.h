@@ -81,6 +81,14 @@ int ga_problem_fill(ga_ctx* ctx, int32_t flags, int64_t* cost_out, int32_t* full
 int ga_problem_traceback(ga_ctx* ctx, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* out_a,
                          char* out_mid, char* out_b, int64_t cap, int64_t* out_len, int32_t* tb_status);
 
+/* Use a caller-filled cell array for the next ga_problem_traceback instead of
+ * a fill: cells = 3*(m+1)*(n+1) int32 (M, X, Y), row-major, boundary
+ * included (the loaded problem's row0/col0 must be its row 0 / column 0).
+ * Replaces the part of dp_array_backward (globaligner.py:425-514) that reads
+ * the caller's dp_array: the walk then follows THOSE cells, whatever filled
+ * them.  *cost_out = min(cells[m][n]).  Small problems only. */
+int ga_problem_set_cells(ga_ctx* ctx, const int32_t* cells, int64_t* cost_out);
+
 /* fill + traceback in one call, overlapping the host-side tie-break table
  * with the device fill (the whole find_global_alignment hot path,
  * globaligner.py:258-302). */

@@ -277,7 +277,8 @@ def test_tall_narrow_vs_oracle(ga):
 def test_bench_workload_cost_matches_golden(ga, name):
     """Each bench.py workload at its full BASELINE size (C4 = 10^12 cells, score only) against the cost
     the threaded C oracle produced (tests/golden/make_cost_golden.py, make_c4_golden.py); traceback
-    workloads also walk and must reproduce both inputs."""
+    workloads also walk, must reproduce both inputs, and must equal the oracle's alignment strings and
+    final random state (tests/golden/make_aln_golden.py: <name>_aln.json digests, random.seed(0))."""
     import bench
     from globalign_amd import _native
     wl = bench.WORKLOADS[name]
@@ -290,8 +291,15 @@ def test_bench_workload_cost_matches_golden(ga, name):
         if wl["traceback"]:
             random.seed(0)
             mt = np.array(random.getstate()[1], dtype=np.uint32)
-            cost, (a, _, b), status, _ = eng.align(mt, s1, s2)
+            cost, (a, mid, b), status, mt_after = eng.align(mt, s1, s2)
             assert status == 0 and a.replace("-", "") == s1 and b.replace("-", "") == s2
+            pin = os.path.join(GOLDEN, f"{name}_aln.json")
+            if os.path.exists(pin):
+                g = json.load(open(pin))
+                st = random.getstate()
+                assert len(mid) == g["aln_len"]
+                assert aln_digest(a, mid, b) == g["aln_sha16"]
+                assert state_digest((st[0], tuple(int(x) for x in mt_after), st[2])) == g["state_sha32"]
         else:
             cost = eng.fill(traceback=False)[0]
     finally:
