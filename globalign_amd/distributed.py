@@ -246,21 +246,72 @@ def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_
     dist.gather_object(seg, segs, dst=0, group=ctrl)
     if rank != 0:
         return None
+    return assemble(segs, state, cost, engine, seq_1, seq_2)
+
+
+def assemble(segs, state, cost, engine, seq_1, seq_2):
+    """The whole alignment from the slabs' walk segments (segs[k]: slab k's columns in walk order) and
+    the final walk state: concatenate right to left, append the reference's tails, reverse
+    (dp_array_backward's end, globaligner.py:542-593).  -> (cost, strings, status, mt_words_after)."""
     i, j, D, reason = state[0], state[1], state[2], state[6]
     mt_after = engine.slab_mt_state(D)
     if reason == 4:
         return cost, ("", "", ""), 1, mt_after
-    parts_a = [s[0] for s in reversed(segs)]
-    parts_m = [s[1] for s in reversed(segs)]
-    parts_b = [s[2] for s in reversed(segs)]
-    sa, sm, sb = "".join(parts_a), "".join(parts_m), "".join(parts_b)
+    sa = "".join(s[0] for s in reversed(segs))
+    sm = "".join(s[1] for s in reversed(segs))
+    sb = "".join(s[2] for s in reversed(segs))
     if reason == 1:  # walk hit row 0: the rest of seq_2 against gaps
-        tail = seq_2[:j][::-1]
-        sa, sm, sb = sa + "-" * j, sm + " " * j, sb + tail
-    elif reason == 2:
-        tail = seq_1[:i][::-1]
-        sa, sm, sb = sa + tail, sm + " " * i, sb + "-" * i
+        sa, sm, sb = sa + "-" * j, sm + " " * j, sb + seq_2[:j][::-1]
+    elif reason == 2:  # walk hit column 0: the rest of seq_1 against gaps
+        sa, sm, sb = sa + seq_1[:i][::-1], sm + " " * i, sb + "-" * i
     return cost, (sa[::-1], sm[::-1], sb[::-1]), 0, mt_after
+
+
+def align_devices(devices, seq_1, seq_2, a_codes, b_codes, tables, mt_words, traceback=True, timeout_s=600.0):
+    """One problem over several GPUs of THIS process (GlobalAligner(devices=[...])): one context and one
+    column slab per device, the slab edges in pinned host memory that both neighbours map, and this
+    thread relaying each slab's right-edge progress word to its right neighbour while the fills run.
+    The same slab protocol as the one-process-per-GPU path (align_slabs) without a process group.
+    -> (cost, strings or None, status, mt_words_after or None)."""
+    import torch
+    world = len(devices)
+    m, n = len(a_codes), len(b_codes)
+    edges = slab_bounds(n, world)
+    engines = [GpuSlabEngine(d) for d in devices]
+    halos = [torch.empty((m + 1, 2), dtype=torch.int32, pin_memory=True) for _ in range(world - 1)]
+    for k, eng in enumerate(engines):
+        eng.load_slab(a_codes, b_codes, tables, edges[k], edges[k + 1])
+        eng.slab_bind_halos(halos[k - 1].data_ptr() if k > 0 else 0, halos[k].data_ptr() if k < world - 1 else 0)
+    # left to right: a slab only ever waits on slabs launched before it (slabs sharing a GPU run in turn)
+    for eng in engines:
+        eng.slab_launch(traceback=traceback)
+    if traceback:
+        engines[-1].slab_walk_prepare(mt_words)  # the host tie-break table, while the fills run
+    relayed = [0] * (world - 1)
+    t0 = time.monotonic()
+    while any(r < m for r in relayed):
+        moved = False
+        for k in range(world - 1):
+            p = min(engines[k].out_progress(), m)
+            if p > relayed[k]:
+                engines[k + 1].set_in_progress(p)
+                relayed[k] = p
+                moved = True
+        if not moved:
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError(f"slab edges stalled at {relayed} of {m} rows")
+            time.sleep(20e-6)
+    costs = [eng.slab_finish() for eng in engines]
+    cost = costs[-1]
+    if not traceback:
+        return cost, None, 0, None
+    for eng in engines[:-1]:
+        eng.slab_walk_prepare(mt_words)
+    state, segs = [m, n, 0, 0, 0, 1, -1], [("", "", "")] * world
+    for k in range(world - 1, -1, -1):
+        if state[6] in (-1, 5):
+            segs[k], state = engines[k].slab_walk(state, seq_1, seq_2)
+    return assemble(segs, state, cost, engines[0], seq_1, seq_2)
 
 
 class GpuSlabEngine:

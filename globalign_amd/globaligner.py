@@ -41,35 +41,58 @@ def _set_mt_words(words):
 
 
 class GlobalAligner:
-    """Reusable aligner bound to one GPU.
+    """Reusable aligner on one GPU or several.
 
     ``GlobalAligner(**settings).align(seq_1, seq_2)`` accepts the same keyword
     settings as find_global_alignment (scores, costs, matrix name/path, gap
     options) and returns an AlignmentResults.  ``max_seq_len_prod=None``
     lifts the reference's m*n < 2e7 API cap (the device path is sized for
     100k x 100k and beyond); ``traceback=False`` returns the score only.
+    ``devices=[0, 1, ...]`` cuts seq_2's columns into one slab per listed GPU
+    of this process (distributed.align_devices: the slab edges stream through
+    mapped host memory while the fills run, the walk is handed right to left);
+    the result is identical to the one-GPU result.  For one process per GPU
+    use globalign_amd.distributed (torch.distributed / RCCL).
     """
 
     def __init__(self, scoring_mat_name=None, scoring_mat_path=None, match_score=None, mismatch_score=None,
                  mismatch_cost=None, gap_open_score=None, gap_open_cost=None, gap_extension_score=None,
-                 gap_extension_cost=None, device=0, max_seq_len_prod=MAX_SEQ_LEN_PROD, traceback=True):
+                 gap_extension_cost=None, device=0, max_seq_len_prod=MAX_SEQ_LEN_PROD, traceback=True, devices=None):
         self.settings = dict(scoring_mat_name=scoring_mat_name, scoring_mat_path=scoring_mat_path,
                              match_score=match_score, mismatch_score=mismatch_score, mismatch_cost=mismatch_cost,
                              gap_open_score=gap_open_score, gap_open_cost=gap_open_cost,
                              gap_extension_score=gap_extension_score, gap_extension_cost=gap_extension_cost)
-        self.device = device
+        self.devices = [int(d) for d in devices] if devices is not None else [int(device)]
+        if not self.devices:
+            raise ValueError("devices must name at least one GPU")
+        self.device = self.devices[0]
         self.max_seq_len_prod = max_seq_len_prod
         self.traceback = traceback
 
     def align(self, seq_1=None, seq_2=None, input_fasta=None, output=None):
         good = validate_and_transform_args(input_fasta, output, seq_1, seq_2, max_seq_len_prod=self.max_seq_len_prod,
                                            **self.settings)
-        return _align_validated(good, device=self.device, traceback=self.traceback)
+        return _align_validated(good, device=self.device, traceback=self.traceback, devices=self.devices)
 
 
-def _align_validated(good, device=0, traceback=True):
+def _align_validated(good, device=0, traceback=True, devices=None):
     seq_1, seq_2, scoring_mat, costing_mat, gap_open_score, gap_open_cost, output = good
     tables = _native.CostTables(costing_mat, gap_open_cost)
+    if devices is not None and len(devices) > 1 and min(len(seq_1), len(seq_2)) >= 2 and len(seq_2) >= len(devices):
+        from . import distributed
+        cost, strings, status, mt = distributed.align_devices(devices, seq_1, seq_2, tables.codes(seq_1),
+                                                              tables.codes(seq_2), tables, _mt_words(),
+                                                              traceback=traceback)
+        if traceback:
+            _set_mt_words(mt)
+            if status == _native.GA_TB_INDEX_ERROR:
+                raise IndexError("string index out of range")
+            a, mid, b = strings
+        else:
+            a = mid = b = None
+        score = final_cost_to_score(cost=cost, m=len(seq_1), n=len(seq_2), max_score=get_max_val(scoring_mat))
+        return AlignmentResults(a, mid, b, cost, score, scoring_mat, costing_mat, gap_open_score, gap_open_cost,
+                                output)
     eng = _native.default_engine(device)
     eng.load(tables.codes(seq_1), tables.codes(seq_2), tables)
     if traceback:

@@ -22,6 +22,13 @@ def final_score_to_cost(score, m, n, max_score, delta_d=None, delta_i=None):
     return -score + n * dd + m * di
 
 
+def print_nested_list_aligned(nested_list):
+    """Print a list of equal-length rows with every column right-aligned to its widest cell + 1
+    (conclude.py:204-249)."""
+    widths = [max(len(str(row[j])) for row in nested_list) for j in range(len(nested_list[0]))]
+    print("".join("".join(f"{str(c):>{w + 1}}" for c, w in zip(row, widths)) + "\n" for row in nested_list))
+
+
 def prettify_mat(mat):
     """Right-aligned text table of a nested-dict matrix with row and column headers."""
     try:

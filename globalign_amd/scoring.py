@@ -330,3 +330,13 @@ def validate_and_transform_args(input_fasta=None, output=None, seq_1=None, seq_2
                                   scores.gap_extension_score)
         cmat = scoring_mat_to_costing_mat(smat, scores.match_score)
     return s1, s2, smat, cmat, scores.gap_open_score, costs.gap_open_cost, out_path
+
+
+def make_matrix(num_rows, num_cols, fill_val):
+    """num_rows independent rows of num_cols copies of fill_val (start.py:869-876)."""
+    return [[fill_val] * num_cols for _ in range(num_rows)]
+
+
+def make_3d_array(dim_1, dim_2, dim_3, fill_val):
+    """dim_1 x dim_2 x dim_3 nested lists of fill_val (start.py:878-881)."""
+    return [[[fill_val] * dim_3 for _ in range(dim_2)] for _ in range(dim_1)]

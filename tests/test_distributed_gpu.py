@@ -111,3 +111,28 @@ def test_gpu_slabs_score_only_diag_match_oracle(td, monkeypatch, tmp_path):
     monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
     test_gpu_slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
     test_gpu_slabs_score_only_match_oracle(3, 12_000, 2_000 + 5, 47 + td, 2048, tmp_path)
+
+
+@pytest.mark.parametrize("devices,m,n,seed,kw", [
+    ([0, 0], 2500, 4100, 41, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+    ([0, 0, 0], 1800, 3000, 42, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)),
+])
+def test_global_aligner_devices_in_process(devices, m, n, seed, kw):
+    """GlobalAligner(devices=[...]): one context and slab per listed GPU in this process (slabs sharing the
+    one MI355X here run in turn), the result bit-exact with the oracle, the random state included."""
+    import globalign_amd
+    from oracle import core, transform
+    from tests.conftest import load_matrix
+    alpha = "protein" if "scoring_mat_name" in kw else "dna"
+    s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
+    blosum = load_matrix(kw["scoring_mat_name"]) if "scoring_mat_name" in kw else None
+    a1, a2, _, cmat, _, goc = transform.settings(dict(kw, seq_1=s1, seq_2=s2), blosum=blosum)
+    random.seed(seed)
+    ref = core.align(a1, a2, cmat, goc, core.mt_state_array())
+    random.seed(seed)
+    r = globalign_amd.GlobalAligner(max_seq_len_prod=None, devices=devices, **kw).align(s1, s2)
+    assert r.cost == ref["cost"]
+    assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == tuple(ref["strings"])
+    assert random.getstate()[1] == tuple(int(x) for x in ref["mt_out"])
+    r2 = globalign_amd.GlobalAligner(max_seq_len_prod=None, devices=devices, traceback=False, **kw).align(s1, s2)
+    assert r2.cost == ref["cost"] and r2.seq_1_aligned is None
