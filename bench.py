@@ -64,8 +64,8 @@ MULTI_GPU_DEFAULT = "c4"
 
 # committed profiles the roofline block is built from: PMC bytes and VALU
 # instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
-TRAFFIC_FILES = {"c3": "traffic.json", "c4": "traffic_c4.json"}
-VALU_FILES = {"c3": "valu_c3.json", "c4": "valu_c4.json"}
+TRAFFIC_FILES = {"c3": "r02/traffic_c3.json", "c4": "r02/traffic_c4.json"}
+VALU_FILES = {"c3": "r02/valu_c3.json", "c4": "r02/valu_c4.json"}
 VALU_MIX_FILES = {"c3": "r02/valu_mix_c3.json", "c4": "r02/valu_mix_c4.json"}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
@@ -208,8 +208,13 @@ def roofline(workload, wl, fill_ms, kernel="fill_kernel"):
 
 
 # ----------------------------------------------------------------------------- single GPU
-def measure_single(wl, steps, warmup):
-    """Time `steps` passes of the hot path over one resident pair on cuda:0."""
+def measure_single(wl, steps, warmup, pipelined=True):
+    """Time `steps` passes of the hot path over one resident pair on cuda:0.
+
+    Traceback workloads: the `steps` alignments are consecutive find_global_alignment-equivalent calls
+    (each starts from the random state the previous left, from random.seed(0)), run through
+    ga_problem_align_many: the walk of alignment k overlaps the fill of alignment k+1 on the GPU.  The
+    single-alignment latency (fill + table + walk + strings, nothing overlapped) is measured separately."""
     import random
     import torch
     from globalign_amd import _native
@@ -219,37 +224,65 @@ def measure_single(wl, steps, warmup):
     eng.load(tables.codes(s1), tables.codes(s2), tables)
     random.seed(0)
     mt0 = np.array(random.getstate()[1], dtype=np.uint32)
-    fill_ms, walk_ms, rng_ms = [], [], []
-    result = None
-
-    def step():
-        if wl["traceback"]:
-            return eng.align(mt0, s1, s2)
-        return eng.fill(traceback=False)
-
-    for _ in range(warmup):
-        result = step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        result = step()
-        tm = eng.timings()
-        fill_ms.append(tm["fill_ms"])
-        walk_ms.append(tm["walk_ms"] if wl["traceback"] else 0.0)
-        rng_ms.append(tm["rng_ms"] if wl["traceback"] else 0.0)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    cost = result[0]
     out = {}
-    if wl["traceback"]:
-        _, (a, mid, b), status, mt_after = result
-        assert status == 0 and a.replace("-", "") == s1 and b.replace("-", "") == s2
+    if wl["traceback"] and pipelined:
+        if warmup:
+            eng.align_many(mt0, s1, s2, warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        runs, mt_after = eng.align_many(mt0, s1, s2, steps)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        tm = eng.timings()
+        fill_ms, walk_ms, rng_ms = tm["fill_ms"], tm["walk_ms"], tm["rng_ms"]
+        cost, (a, mid, b), status = runs[0]
+        for c_k, (a_k, _, b_k), st_k in runs:
+            assert st_k == 0 and c_k == cost and a_k.replace("-", "") == s1 and b_k.replace("-", "") == s2
         out["aln"] = (a, mid, b)
-        out["mt_after"] = mt_after
+        # the state after the FIRST alignment (the pin is for one call from random.seed(0))
+        _, _, _, out["mt_after"] = eng.align(mt0, s1, s2)
+        lat = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            eng.align(mt0, s1, s2)
+            lat.append((time.perf_counter() - t1) * 1e3)
+        out["latency_ms"] = float(min(lat))
+        out["mode"] = "pipelined: walk k beside fill k+1 (ga_problem_align_many)"
+    else:
+        fill_l, walk_l, rng_l = [], [], []
+        result = None
+
+        def step():
+            if wl["traceback"]:
+                return eng.align(mt0, s1, s2)
+            return eng.fill(traceback=False)
+
+        for _ in range(warmup):
+            result = step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            result = step()
+            tm = eng.timings()
+            fill_l.append(tm["fill_ms"])
+            walk_l.append(tm["walk_ms"] if wl["traceback"] else 0.0)
+            rng_l.append(tm["rng_ms"] if wl["traceback"] else 0.0)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        fill_ms, walk_ms, rng_ms = float(np.mean(fill_l)), float(np.mean(walk_l)), float(np.mean(rng_l))
+        cost = result[0]
+        if wl["traceback"]:
+            _, (a, mid, b), status, mt_after = result
+            assert status == 0 and a.replace("-", "") == s1 and b.replace("-", "") == s2
+            out["aln"] = (a, mid, b)
+            out["mt_after"] = mt_after
+            out["latency_ms"] = elapsed * 1e3 / steps
+        out["mode"] = "one call per step"
+    eng.close()
     cells = wl["m"] * wl["n"]
     out.update(elapsed=elapsed, cost=int(cost), cells=cells, value=cells * steps / elapsed,
-               ms_per_step=elapsed * 1e3 / steps, fill_ms=float(np.mean(fill_ms)), walk_ms=float(np.mean(walk_ms)),
-               rng_ms=float(np.mean(rng_ms)))
+               ms_per_step=elapsed * 1e3 / steps, fill_ms=float(fill_ms), walk_ms=float(walk_ms),
+               rng_ms=float(rng_ms))
     return out
 
 
@@ -293,6 +326,8 @@ def single_line(args, workload, wl):
     if wl["traceback"]:
         line["walk_ms"] = r["walk_ms"]
         line["host_tiebreak_ms"] = r["rng_ms"]
+        line["latency_ms_per_alignment"] = r["latency_ms"]
+        line["step_mode"] = r["mode"]
         line["config"]["traceback_pin"] = traceback_pin(workload, r)
     if workload == SINGLE_GPU_DEFAULT and not args.no_extra:
         # one GPU's point of BASELINE's C4 scaling curve (the same pair bench.py --gpus N slabs)

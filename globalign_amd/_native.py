@@ -40,7 +40,7 @@ class EngineError(RuntimeError):
 # every symbol include/globalign_amd.h declares (tests check the exports)
 EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
-    "ga_problem_traceback", "ga_problem_align", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
+    "ga_problem_traceback", "ga_problem_align", "ga_problem_align_many", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
     "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_ctx_wait_stream", "ga_ctx_stream_priority",
     "ga_last_kernel_ms", "ga_last_timings",
@@ -105,6 +105,8 @@ def load_library():
                                            pi64, p32]
         L.ga_problem_align.argtypes = [vp, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i64,
                                        pi64, p32, pi64]
+        L.ga_problem_align_many.argtypes = [vp, i32, pu32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                            C.c_char_p, i64, pi64, p32, pi64]
         L.ga_problem_set_slab.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), i64, i64]
         L.ga_slab_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
         L.ga_slab_bind_halos.argtypes = [vp, vp, vp]
@@ -243,6 +245,28 @@ class Engine:
         cost = C.c_int64(0)
         strings, st, mt = self._tb_call(self._L.ga_problem_align, mt_words, a_chr, b_chr, (C.byref(cost),))
         return cost.value, strings, st, mt
+
+    def align_many(self, mt_words, a_chr, b_chr, count):
+        """`count` consecutive alignments of the loaded pair, each from the random state the previous one left
+        (as consecutive find_global_alignment calls); walk k overlaps fill k+1 on the device.
+        -> ([(cost, strings, status)] * count, mt_words_after)"""
+        mt = np.ascontiguousarray(mt_words, dtype=np.uint32).copy()
+        cap = self.m + self.n + 2
+        oa, om, ob = (C.create_string_buffer(cap * count) for _ in range(3))
+        ln = np.zeros(count, dtype=np.int64)
+        st = np.zeros(count, dtype=np.int32)
+        cost = np.zeros(count, dtype=np.int64)
+        p64, p32 = C.POINTER(C.c_int64), C.POINTER(C.c_int32)
+        _check(self._L.ga_problem_align_many(self._h, int(count), mt.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                             a_chr.encode(), b_chr.encode(), oa, om, ob, cap, ln.ctypes.data_as(p64),
+                                             st.ctypes.data_as(p32), cost.ctypes.data_as(p64)))
+        out = []
+        ra, rm, rb = oa.raw, om.raw, ob.raw
+        for k in range(count):
+            lo, L = k * cap, int(ln[k])
+            out.append((int(cost[k]), (ra[lo:lo + L].decode(), rm[lo:lo + L].decode(), rb[lo:lo + L].decode()),
+                        int(st[k])))
+        return out, mt
 
     def timings(self):
         """{fill_ms, walk_ms, rng_ms (host tie-break table), call_ms} of the last call."""

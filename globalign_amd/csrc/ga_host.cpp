@@ -158,12 +158,8 @@ struct Quad2 {
     }
 };
 
-struct RngTable {
-    std::vector<uint32_t> tab;        // per dispatch: level per candidate set (see dispatch_entry)
-    std::vector<uint32_t> step_end;   // words consumed after each dispatch
-    std::vector<PyMT> twist_snap;     // MT array after every 64th twist (index 0 = initial state)
-    int mti0 = 0;
-};
+struct RngTable;
+void fill_entries(const uint8_t* acc, int64_t from, int64_t to, RngTable& R);
 
 constexpr int TWSNAP = 64;
 
@@ -178,9 +174,91 @@ inline void temper_block(const uint32_t* mt, uint32_t* out) {
     }
 }
 
+// The tie-break table as a RESUMABLE stream over CPython's MT19937 words: extend(D) makes the
+// entries of dispatches [0, D) available, continuing where the last call stopped.  Consecutive
+// alignments (each a find_global_alignment call that starts from the state the previous one left)
+// consume ONE continuous stream of accepted draws, 18 per dispatch, so alignment k's dispatches are
+// the global dispatches [G_k, G_k + D_k) of the same table (ga_problem_align_many).
+struct RngTable {
+    std::vector<uint32_t> tab;        // per dispatch: level per candidate set (see fill_entries)
+    std::vector<uint32_t> step_end;   // words consumed after each dispatch
+    std::vector<PyMT> twist_snap;     // MT array after every 64th twist (index 0 = initial state)
+    int mti0 = 0;
+    // stream position
+    PyMT g{};
+    uint32_t words[MTN + 4]{};
+    int q = 0, count = 0;             // next word of the current tempered block, words in it
+    int64_t wbase = 0, ntw = 0, p = 0, stp = 0;
+    unsigned d = 0;                   // draw index within the dispatch (0..17)
+    std::vector<uint8_t> acc;         // accepted draws (values 0..2)
+    int64_t built = 0;                // dispatches whose entries are in tab
+
+    void start(const uint32_t* state) {
+        std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
+        g.mti = (int)state[MTN];
+        mti0 = g.mti;
+        twist_snap.assign(1, g);
+        tab.clear();
+        step_end.clear();
+        acc.clear();
+        wbase = ntw = p = stp = built = 0;
+        d = 0;
+        // the partial first block: words mti0 .. 623 of the initial array
+        uint32_t tmp[MTN];
+        temper_block(g.mt, tmp);
+        const int first = g.mti >= MTN ? 0 : g.mti;
+        count = g.mti >= MTN ? 0 : MTN - g.mti;
+        std::memcpy(words, tmp + first, sizeof(uint32_t) * count);
+        q = 0;
+    }
+
+    void extend(int64_t steps) {
+        if (steps <= built) return;
+        static const Quad2 Q;
+        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
+        const int64_t need = 18 * steps;
+        acc.resize(need + 8);
+        step_end.resize(steps + 4);
+        while (p < need) {
+            if (q >= count) {
+                wbase += count;
+                g.twist();
+                ntw++;
+                if (ntw % TWSNAP == 0) twist_snap.push_back(g);
+                temper_block(g.mt, words);
+                count = MTN;
+                q = 0;
+            }
+            for (; q + 4 <= count && p < need; q += 4) {
+                const unsigned B = (words[q] >> 30) | ((words[q + 1] >> 30) << 2) | ((words[q + 2] >> 30) << 4) |
+                                   ((words[q + 3] >> 30) << 6);
+                const QuadEntry2& e = Q.e[d][B];
+                std::memcpy(acc.data() + p, &e.bytes, 4);
+                step_end[stp] = (uint32_t)(wbase + q + e.woff);  // branch-free: kept only when a dispatch completes
+                stp += e.wrap;
+                p += e.nacc;
+                d = e.nd;
+            }
+            // tail words of the block (count not a multiple of 4), one at a time
+            for (; q + 4 > count && q < count && p < need; q++) {
+                const unsigned r = words[q] >> 30;
+                if (r < sz[d]) {
+                    acc[p] = (uint8_t)r;
+                    if (d == 17) step_end[stp++] = (uint32_t)(wbase + q + 1);
+                    p++;
+                    d = d == 17 ? 0 : d + 1;
+                }
+            }
+        }
+        tab.resize(steps);
+        fill_entries(acc.data(), built, steps, *this);
+        built = steps;
+    }
+};
+
 // The per-step entries from the accepted draws (18 per dispatch; draws 0-3 / 9-12 decide).
-void fill_entries(const uint8_t* acc, int64_t steps, RngTable& R) {
-    for (int64_t st = 0; st < steps; st++) {
+void fill_entries(const uint8_t* acc, int64_t from, int64_t to, RngTable& R) {
+    for (int64_t st = from; st < to; st++) {
         const uint8_t* r = acc + 18 * st;
         uint32_t e = 0;
         for (int half = 0; half < 2; half++) {
@@ -197,63 +275,8 @@ void fill_entries(const uint8_t* acc, int64_t steps, RngTable& R) {
 // tempering the stream is the cost (~9 ms for 2*10^5 dispatches on an EPYC 9575F); it runs
 // while the device fills.  (A producer/consumer split over two threads measured no faster.)
 void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
-    static const Quad2 Q;
-    PyMT g;
-    std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
-    g.mti = (int)state[MTN];
-    R.mti0 = g.mti;
-    R.twist_snap.clear();
-    R.twist_snap.push_back(g);
-    R.tab.assign(steps, 0);
-    const int64_t need = 18 * steps;
-    std::vector<uint8_t> acc(need + 8);
-    std::vector<uint32_t> ends(steps + 4);
-    int64_t stp = 0;
-    uint32_t words[MTN + 4];
-    int64_t p = 0, wbase = 0, ntw = 0;
-    unsigned d = 0;
-    // the partial first block: words mti0 .. 623 of the initial array
-    int first = g.mti, count = MTN - g.mti;
-    if (g.mti >= MTN) { count = 0; first = 0; }
-    uint32_t tmp[MTN];
-    temper_block(g.mt, tmp);
-    std::memcpy(words, tmp + first, sizeof(uint32_t) * count);
-    while (p < need) {
-        if (count == 0) {
-            g.twist();
-            ntw++;
-            if (ntw % TWSNAP == 0) R.twist_snap.push_back(g);
-            temper_block(g.mt, words);
-            count = MTN;
-        }
-        int q = 0;
-        for (; q + 4 <= count && p < need; q += 4) {
-            const unsigned B = (words[q] >> 30) | ((words[q + 1] >> 30) << 2) | ((words[q + 2] >> 30) << 4) |
-                               ((words[q + 3] >> 30) << 6);
-            const QuadEntry2& e = Q.e[d][B];
-            std::memcpy(acc.data() + p, &e.bytes, 4);
-            ends[stp] = (uint32_t)(wbase + q + e.woff);  // branch-free: kept only when a dispatch completes
-            stp += e.wrap;
-            p += e.nacc;
-            d = e.nd;
-        }
-        // tail words of the block (count not a multiple of 4), one at a time
-        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
-        for (; q < count && p < need; q++) {
-            const unsigned r = words[q] >> 30;
-            if (r < sz[d]) {
-                acc[p] = (uint8_t)r;
-                if (d == 17) ends[stp++] = (uint32_t)(wbase + q + 1);
-                p++;
-                d = d == 17 ? 0 : d + 1;
-            }
-        }
-        wbase += count;
-        count = 0;
-    }
-    ends.resize(steps);
-    R.step_end = std::move(ends);
-    fill_entries(acc.data(), steps, R);
+    R.start(state);
+    R.extend(steps);
 }
 
 // MT state after the first D dispatches consumed their words.
@@ -314,6 +337,17 @@ struct ga_ctx {
     int2* halo_in_ext = nullptr;   // caller-bound halo buffers (e.g. tensors RCCL sends from / receives into)
     int2* halo_out_ext = nullptr;
     RngTable walk_rng;             // tie-break table of the global problem (slab walks)
+    // pipelined repeated alignments (ga_problem_align_many): two slots of traceback words, walk
+    // buffers and events; the walk runs on its own stream beside the next fill
+    struct PipeSlot {
+        DevBuf tb, rng, ops, result;
+        hipEvent_t f0 = nullptr, f1 = nullptr, fdone = nullptr, w0 = nullptr, w1 = nullptr;
+        uint32_t* tab_pin = nullptr;  // pinned staging of the walk's table slice
+        int64_t tab_cap = 0;
+    } pipe[2];
+    hipStream_t wstream = nullptr;
+    int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
+    RngTable many_rng;
     bool walk_rng_ready = false;
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
     bool dbg_on = false;
@@ -468,6 +502,8 @@ struct Band {
     bool band = false;          // fill rows r0+1 .. r0+mb only (the boundary is already computed)
     int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
     int ckpt_rows = 0;
+    DevBuf* tbuf = nullptr;     // traceback words into this buffer instead of ctx->tb (pipelined alignments)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // fill timing events instead of ctx->ev[0 / 1]
 };
 
 // Enqueue boundary + query profile + fill.  Does not synchronise.
@@ -511,7 +547,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         set_stripes(c, c->T_req, tb, full, n);
     }
     // traceback words cover T 64-column stripes per fill stripe
-    if (tb) HIPCHK(c->tb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
+    DevBuf& tbb = bd.tbuf ? *bd.tbuf : c->tb;
+    if (tb) HIPCHK(tbb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
     HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
     // workgroup hand-off rows read by a successor start as ga::HAND_SENT (bytes 0x80)
     if (c->nslabs > 1)
@@ -547,7 +584,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.hand = c->hand.as<int2>();
     p.ticket = fl;
     p.abort_word = fl + 1;
-    p.tb = tb ? c->tb.as<uint8_t>() : nullptr;
+    p.tb = tb ? tbb.as<uint8_t>() : nullptr;
     p.out_last = c->out_last.as<int>();
     p.edge_prog = c->slab ? c->prog_dev + 1 : nullptr;  // [1]: halo_out rows
     p.edge_out = c->slab ? c->halo_out_ext : nullptr;
@@ -565,11 +602,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], c->stream));
     if (c->diag) ga::launch_fill_diag(c->stream, p, c->qbytes, full);
     else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(hipEventRecord(bd.ev1 ? bd.ev1 : c->ev[1], c->stream));
     c->filled_tb = tb;
     return GA_OK;
 }
@@ -625,18 +662,33 @@ struct WalkStart {
     int L, first;
 };
 
+// Where a walk reads its words and table and leaves its levels / result, on which stream.
+struct WalkBufs {
+    const uint8_t* tb;
+    uint32_t* rng;
+    uint32_t* ops;
+    int* result;
+    hipStream_t stream;
+    hipEvent_t ev0, ev1;
+};
+WalkBufs ctx_walk_bufs(ga_ctx* c) {
+    return WalkBufs{c->tb.as<uint8_t>(), c->rng.as<uint32_t>(), c->ops.as<uint32_t>(), c->result.as<int>(), c->stream,
+                    c->ev[2], c->ev[3]};
+}
+
 int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, int64_t r0 = 0, int64_t mb = -1,
-             bool vhandoff = false, bool upload_tab = true) {
-    if (upload_tab) HIPCHK(hipMemcpyAsync(c->rng.p, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, c->stream));
+             bool vhandoff = false, bool upload_tab = true, const WalkBufs* wbp = nullptr) {
+    const WalkBufs wb = wbp ? *wbp : ctx_walk_bufs(c);
+    if (upload_tab) HIPCHK(hipMemcpyAsync(wb.rng, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
     ga::WalkArgs w{};
-    w.tb = c->tb.as<uint8_t>();
+    w.tb = wb.tb;
     w.CB = c->CB;
     w.TC = c->TC;
     w.a = c->a.as<uint8_t>() + r0;
     w.b = c->b.as<uint8_t>() + c->col0;
     w.bnd_row = c->bnd_row.as<int>() + 3 * c->col0;
     w.bnd_col = c->bnd_col.as<int>() + 3 * r0;
-    w.rng = c->rng.as<uint32_t>();
+    w.rng = wb.rng;
     w.nrng = (long long)ntab;
     w.m = (int)(mb >= 0 ? mb : c->m);
     w.n = (int)c->n;
@@ -650,17 +702,17 @@ int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, 
     w.h0 = (int)st.h;
     w.handoff = c->col0 > 0;
     w.maxh = (int)(c->m + c->n_global);
-    w.ops = c->ops.as<uint32_t>();
-    w.result = c->result.as<int>();
+    w.ops = wb.ops;
+    w.result = wb.result;
     if (c->dbg_on) {
         HIPCHK(c->wdbg.ensure(sizeof(unsigned) * 4 * 8192));
-        HIPCHK(hipMemsetAsync(c->wdbg.p, 0xff, sizeof(unsigned) * 4 * 8192, c->stream));
+        HIPCHK(hipMemsetAsync(c->wdbg.p, 0xff, sizeof(unsigned) * 4 * 8192, wb.stream));
     }
     w.dbg = c->dbg_on ? c->wdbg.as<unsigned>() : nullptr;
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
-    ga::launch_walk(c->stream, w);
+    HIPCHK(hipEventRecord(wb.ev0, wb.stream));
+    ga::launch_walk(wb.stream, w);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    HIPCHK(hipEventRecord(wb.ev1, wb.stream));
     return GA_OK;
 }
 
@@ -669,10 +721,11 @@ inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 // Wait for the walk; decode the levels of dispatches [st.D, D_end) into alignment columns in walk
 // order starting at (st.i, st.j) (global columns).  Returns the end state through `st` and `reason`.
 int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const char* b_chr, char* oa, char* om,
-                 char* ob, int64_t cap, int64_t& len) {
+                 char* ob, int64_t cap, int64_t& len, const WalkBufs* wbp = nullptr) {
+    const WalkBufs wb = wbp ? *wbp : ctx_walk_bufs(c);
     int res[16];
-    HIPCHK(hipMemcpyAsync(res, c->result.p, sizeof(int) * 16, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpyAsync(res, wb.result, sizeof(int) * 16, hipMemcpyDeviceToHost, wb.stream));
+    HIPCHK(hipStreamSynchronize(wb.stream));
     c->walk_waits = res[4];
     c->walk_tiles = res[5];
     c->walk_t_tile = res[6];
@@ -681,14 +734,15 @@ int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const
     c->walk_c_total = res[9];
     c->walk_load_ticks = res[10];
     c->walk_load_count = res[11];
-    HIPCHK(hipEventElapsedTime(&c->walk_ms, c->ev[2], c->ev[3]));
+    HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
     const int64_t D0 = st.D, D1 = res[0];
     reason = res[3];
     // levels are packed 2 bits per dispatch, dispatch k at bits 30 - 2*(k & 15) of u32 word k >> 4
     const int64_t w0 = D0 >> 4, w1 = (D1 + 15) >> 4;
     std::vector<uint32_t> ops((size_t)std::max<int64_t>(w1 - w0, 0));
     if (D1 > D0)
-        HIPCHK(hipMemcpy(ops.data(), c->ops.as<uint32_t>() + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(ops.data(), wb.ops + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, wb.stream));
+    HIPCHK(hipStreamSynchronize(wb.stream));
     const int64_t m = c->m, n = c->n_global;
     int64_t i = st.i, j = st.j;
     int L = st.L;
@@ -737,7 +791,7 @@ int finish_walk(ga_ctx* c, const RngTable& snaps, uint32_t* mt_state, const char
 int conclude_walk(const RngTable& snaps, const WalkStart& st, int reason, uint32_t* mt_state, const char* a_chr,
                   const char* b_chr, char* oa, char* om, char* ob, int64_t cap, int64_t len, int64_t* out_len,
                   int32_t* tb_status) {
-    state_after(snaps, st.D, mt_state);
+    if (mt_state) state_after(snaps, st.D, mt_state);
     if (reason == 4) {  // IndexError in the reference
         *tb_status = GA_TB_INDEX_ERROR;
         *out_len = 0;
@@ -841,6 +895,113 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
     return rc;
 }
 
+// ---------------------------------------------------------------- pipelined repeated alignments
+int pipe_setup(ga_ctx* c) {
+    if (!c->wstream) HIPCHK(hipStreamCreateWithPriority(&c->wstream, hipStreamNonBlocking, c->priority));
+    if (!c->pipe_pin) {
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 16, hipHostMallocDefault));
+        c->pipe_pin = static_cast<int*>(hp);
+    }
+    const int64_t per = c->m + c->n + 1;
+    for (auto& sl : c->pipe) {
+        for (hipEvent_t* e : {&sl.f0, &sl.f1, &sl.w0, &sl.w1})
+            if (!*e) HIPCHK(hipEventCreate(e));
+        if (!sl.fdone) HIPCHK(hipEventCreateWithFlags(&sl.fdone, hipEventDisableTiming));
+        if (sl.tab_cap < per) {
+            if (sl.tab_pin) HIPCHK(hipHostFree(sl.tab_pin));
+            void* hp = nullptr;
+            HIPCHK(hipHostMalloc(&hp, sizeof(uint32_t) * per, hipHostMallocDefault));
+            sl.tab_pin = static_cast<uint32_t*>(hp);
+            sl.tab_cap = per;
+        }
+        HIPCHK(sl.rng.ensure(sizeof(uint32_t) * per));
+        HIPCHK(sl.ops.ensure(c->m + c->n + 1024));
+        HIPCHK(sl.result.ensure(sizeof(int) * 16));
+    }
+    return GA_OK;
+}
+
+// fill of alignment k into slot k & 1, then its cost inputs into pinned memory, then `fdone`
+int pipe_fill(ga_ctx* c, int slot) {
+    auto& sl = c->pipe[slot];
+    Band bd;
+    bd.tbuf = &sl.tb;
+    bd.ev0 = sl.f0;
+    bd.ev1 = sl.f1;
+    if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
+    int* pin = c->pipe_pin + 8 * slot;
+    HIPCHK(hipMemcpyAsync(pin, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(pin + 4, c->meta.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(pin + 5, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(pin + 6, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipEventRecord(sl.fdone, c->stream));
+    return GA_OK;
+}
+
+int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
+               char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const double t0 = now_ms();
+    if (int r = pipe_setup(c)) return r;
+    const int64_t m = c->m, n = c->n, per = m + n + 1;
+    if (int r = pipe_fill(c, 0)) return r;
+    RngTable& R = c->many_rng;  // one continuous stream for all `count` alignments
+    double rng_ms = 0.0;
+    {
+        const double t1 = now_ms();
+        R.start(mt_state);
+        R.extend(per);
+        rng_ms += now_ms() - t1;
+    }
+    int64_t G = 0;  // global dispatches consumed by the alignments before k
+    float fill_sum = 0.f, walk_sum = 0.f;
+    for (int k = 0; k < count; k++) {
+        auto& sl = c->pipe[k & 1];
+        // walk k: after fill k, on the walk stream, over its table slice [G, G + per)
+        HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
+        std::memcpy(sl.tab_pin, R.tab.data() + G, sizeof(uint32_t) * per);
+        const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
+                          c->wstream, sl.w0, sl.w1};
+        if (int r = run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb)) return r;
+        // fill k+1 into the other slot (after walk k-1, which read it), beside walk k
+        if (k + 1 < count) {
+            auto& nx = c->pipe[(k + 1) & 1];
+            if (k >= 1) HIPCHK(hipStreamWaitEvent(c->stream, nx.w1, 0));
+            if (int r = pipe_fill(c, (k + 1) & 1)) return r;
+            // the table for alignment k+1: G_{k+1} <= G + per, so entries up to G + 2 per
+            const double t1 = now_ms();
+            R.extend(G + 2 * per);
+            rng_ms += now_ms() - t1;
+        }
+        // alignment k's cost and strings
+        HIPCHK(hipEventSynchronize(sl.fdone));
+        const int* pin = c->pipe_pin + 8 * (k & 1);
+        if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+        cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
+        float f = 0.f;
+        if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
+        WalkStart st{m, n, 0, 0, 0, 1};
+        int reason = 0;
+        int64_t len = 0;
+        char* a_k = oa + (size_t)k * cap;
+        char* m_k = om + (size_t)k * cap;
+        char* b_k = ob + (size_t)k * cap;
+        if (int r = walk_segment(c, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, &wb)) return r;
+        walk_sum += c->walk_ms;
+        if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
+                                  &tb_status[k]))
+            return r;
+        G += st.D;
+    }
+    state_after(R, G, mt_state);  // the state the last alignment leaves (random.getstate() layout)
+    c->fill_ms = fill_sum / count;
+    c->walk_ms = walk_sum / count;
+    c->rng_ms = (float)(rng_ms / count);
+    c->call_ms = (float)(now_ms() - t0);
+    c->filled_tb = false;  // ctx->tb does not hold the last fill's words
+    return GA_OK;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -913,6 +1074,14 @@ void ga_ctx_destroy(ga_ctx* c) {
                       &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
+    for (auto& sl : c->pipe) {
+        for (DevBuf* b : {&sl.tb, &sl.rng, &sl.ops, &sl.result}) b->release();
+        for (hipEvent_t e : {sl.f0, sl.f1, sl.fdone, sl.w0, sl.w1})
+            if (e) (void)hipEventDestroy(e);
+        if (sl.tab_pin) (void)hipHostFree(sl.tab_pin);
+    }
+    if (c->pipe_pin) (void)hipHostFree(c->pipe_pin);
+    if (c->wstream) (void)hipStreamDestroy(c->wstream);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_dep) (void)hipEventDestroy(c->ev_dep);
@@ -985,6 +1154,36 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     const int rc = finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
     return rc;
+}
+
+int ga_problem_align_many(ga_ctx* c, int32_t count, uint32_t* mt_state, const char* a_chr, const char* b_chr,
+                          char* oa, char* om, char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status,
+                          int64_t* cost_out) {
+    if (int r = check_ctx(c)) return r;
+    if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
+    if (count < 1) return fail(GA_E_ARG, "count must be >= 1");
+    if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status || !cost_out)
+        return fail(GA_E_ARG, "null argument");
+    if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
+    if (count == 1 || band_rows(c) > 0) {
+        // one alignment, or banded tracebacks (whose band fills hold every CU): one after another
+        const double t0 = now_ms();
+        float fs = 0.f, ws = 0.f, rs = 0.f;
+        for (int k = 0; k < count; k++) {
+            if (int r = ga_problem_align(c, mt_state, a_chr, b_chr, oa + (size_t)k * cap, om + (size_t)k * cap,
+                                         ob + (size_t)k * cap, cap, &out_len[k], &tb_status[k], &cost_out[k]))
+                return r;
+            fs += c->fill_ms;
+            ws += c->walk_ms;
+            rs += c->rng_ms;
+        }
+        c->fill_ms = fs / count;
+        c->walk_ms = ws / count;
+        c->rng_ms = rs / count;
+        c->call_ms = (float)(now_ms() - t0);
+        return GA_OK;
+    }
+    return align_many(c, count, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
 }
 
 // ---------------------------------------------------------------- slabs

@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
         // only the slab's own right edge out to another GPU keeps the progress word
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
         int hlast = h00;  // H' of row in_next of the left edge
-        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
+        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
         while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
             if (q_next < (unsigned)m) {
@@ -465,12 +465,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_kernel(FillArgs p) {
             }
             if (in_next < (unsigned)m && in_sent) {
                 // the contiguous written prefix of the next (up to) 64 rows, as far as ring 0 has space
-                const unsigned cap = min(min(lds_ld(&pc.cons(0)) + RING, (unsigned)m), in_next + 64);
+                const unsigned cap = min(min(lds_ld(&pc.cons(0)) + RING, (unsigned)m), in_next + in_win);
                 if (cap > in_next) {
                     const unsigned r = in_next + 1 + lane;
                     const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
                     const unsigned long long ok = __ballot(e1.x != HAND_SENT);
                     const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;  // rows in_next+1 .. +k
+                    // poll window: the writer publishes GOUT rows at a time, so a waiting reader looks
+                    // at the next 8 rows only; a reader that found its whole window written is behind
+                    // and takes 64 at a time (the full window polled 3.5 GB of unwritten rows per C4 fill)
+                    in_win = k >= cap - in_next ? 64u : 8u;
                     if (k > 0) {
                         // H' of row r-1: the lane before (lane 0: the last row of the previous batch)
                         const int h0 = __builtin_amdgcn_update_dpp(hlast, e1.x, 0x138, 0xf, 0xf, false);
@@ -1004,7 +1008,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
         const int2* rout = ring + nlive * RING;
         const int K = p.K;
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);  // as in fill_kernel
-        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0;
+        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
         while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
             bool moved = false;
             if (q_next < (unsigned)m) {
@@ -1029,12 +1033,13 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_diag_kernel(FillArgs p) {
                 }
             }
             if (in_next < (unsigned)m && in_sent) {
-                const unsigned cap = min(min(lds_ld(cons(0)) + RING, (unsigned)m), in_next + 64);
+                const unsigned cap = min(min(lds_ld(cons(0)) + RING, (unsigned)m), in_next + in_win);
                 if (cap > in_next) {
                     const unsigned r = in_next + 1 + lane;
                     const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
                     const unsigned long long ok = __ballot(e1.x != HAND_SENT);
                     const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;
+                    in_win = k >= cap - in_next ? 64u : 8u;  // poll window (as in fill_kernel)
                     if (k > 0) {
                         if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
                         const unsigned hi = in_next + k;

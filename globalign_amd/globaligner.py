@@ -75,6 +75,33 @@ class GlobalAligner:
         return _align_validated(good, device=self.device, traceback=self.traceback, devices=self.devices)
 
 
+    def align_repeated(self, seq_1, seq_2, count):
+        """`count` alignments of one pair, as `count` consecutive find_global_alignment calls make them: each
+        starts from the global random state the previous one left, so the tie-breaks -- and with them the
+        co-optimal alignment returned -- differ from call to call exactly as in the reference.  On one GPU
+        the walk of alignment k runs beside the fill of alignment k+1 (ga_problem_align_many).
+        -> list of AlignmentResults."""
+        good = validate_and_transform_args(None, None, seq_1, seq_2, max_seq_len_prod=self.max_seq_len_prod,
+                                           **self.settings)
+        s1, s2, scoring_mat, costing_mat, gos, goc, output = good
+        if len(self.devices) > 1 or not self.traceback or min(len(s1), len(s2)) < 2:
+            # (degenerate lengths may raise the reference's IndexError mid-way: one call at a time)
+            return [_align_validated(good, device=self.device, traceback=self.traceback, devices=self.devices)
+                    for _ in range(int(count))]
+        tables = _native.CostTables(costing_mat, goc)
+        eng = _native.default_engine(self.device)
+        eng.load(tables.codes(s1), tables.codes(s2), tables)
+        runs, mt = eng.align_many(_mt_words(), s1, s2, int(count))
+        _set_mt_words(mt)
+        out = []
+        for cost, (a, mid, b), status in runs:
+            if status == _native.GA_TB_INDEX_ERROR:
+                raise IndexError("string index out of range")
+            score = final_cost_to_score(cost=cost, m=len(s1), n=len(s2), max_score=get_max_val(scoring_mat))
+            out.append(AlignmentResults(a, mid, b, cost, score, scoring_mat, costing_mat, gos, goc, output))
+        return out
+
+
 def _align_validated(good, device=0, traceback=True, devices=None):
     seq_1, seq_2, scoring_mat, costing_mat, gap_open_score, gap_open_cost, output = good
     tables = _native.CostTables(costing_mat, gap_open_cost)

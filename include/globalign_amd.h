@@ -96,6 +96,20 @@ int ga_problem_align(ga_ctx* ctx, uint32_t* mt_state, const char* a_chr, const c
                      char* out_mid, char* out_b, int64_t cap, int64_t* out_len, int32_t* tb_status,
                      int64_t* cost_out);
 
+/* `count` consecutive alignments of the loaded pair, exactly as `count`
+ * consecutive find_global_alignment calls make them: alignment k starts from
+ * the random state alignment k-1 left (repeated calls sample the co-optimal
+ * alignments the reference's tie-breaks reach).  The walk of alignment k runs
+ * on a second stream beside the fill of alignment k+1 (double-buffered
+ * traceback words; the tie-break table is one continuous MT19937 stream), so
+ * the throughput is one fill per alignment.  out_a/out_mid/out_b: count*cap
+ * bytes, alignment k at offset k*cap; out_len, tb_status, cost_out: count
+ * entries; mt_state: in the state before the first alignment, out the state
+ * after the last. */
+int ga_problem_align_many(ga_ctx* ctx, int32_t count, uint32_t* mt_state, const char* a_chr, const char* b_chr,
+                          char* out_a, char* out_mid, char* out_b, int64_t cap, int64_t* out_len, int32_t* tb_status,
+                          int64_t* cost_out);
+
 /* ---- multi-GPU column slabs ----------------------------------
  * A context can own the column slab [col_begin, col_end) of a larger problem
  * (global m, n and boundary).  Its left edge arrives in `halo_in`

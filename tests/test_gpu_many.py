@@ -1,0 +1,87 @@
+"""Pipelined repeated alignments (ga_problem_align_many, GlobalAligner.align_repeated) vs the oracle.
+
+`count` alignments of one pair must equal `count` consecutive find_global_alignment calls: alignment k
+starts from the random state alignment k-1 left, so each k has its own tie-breaks.  The oracle runs the
+same chain (core.align with the previous call's final state); strings, costs and every intermediate and
+final random state must agree."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN, aln_digest, load_matrix, splitmix_seq, state_digest
+
+pytestmark = pytest.mark.gpu
+
+
+def _chain_oracle(s1, s2, kw, seed, count):
+    from oracle import core, transform
+    blosum = load_matrix(kw["scoring_mat_name"]) if kw.get("scoring_mat_name") else None
+    a1, a2, _, cmat, _, goc = transform.settings(dict(kw, seq_1=s1, seq_2=s2), blosum=blosum)
+    random.seed(seed)
+    mt = core.mt_state_array()
+    out = []
+    for _ in range(count):
+        r = core.align(a1, a2, cmat, goc, mt)
+        mt = np.asarray(r["mt_out"], dtype=np.uint32)
+        out.append((r["cost"], tuple(r["strings"]), mt.copy()))
+    return out
+
+
+@pytest.mark.parametrize("m,n,seed,count,kw", [
+    (3000, 2500, 7, 4, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+    (1500, 1700, 8, 3, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)),
+    (900, 1000, 9, 2, dict(mismatch_cost=5, gap_open_cost=9, gap_extension_cost=3)),
+    (2000, 64, 10, 5, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+])
+def test_align_repeated_matches_chained_oracle(m, n, seed, count, kw):
+    import globalign_amd
+    alpha = "protein" if "scoring_mat_name" in kw else "dna"
+    s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
+    ref = _chain_oracle(s1, s2, kw, seed, count)
+    random.seed(seed)
+    runs = globalign_amd.GlobalAligner(max_seq_len_prod=None, **kw).align_repeated(s1, s2, count)
+    assert len(runs) == count
+    for r, (cost, strings, _) in zip(runs, ref):
+        assert r.cost == cost
+        assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == strings
+    assert random.getstate()[1] == tuple(int(x) for x in ref[-1][2])
+    # the same as `count` separate calls
+    random.seed(seed)
+    for cost, strings, _ in ref:
+        r = globalign_amd.GlobalAligner(max_seq_len_prod=None, **kw).align(s1, s2)
+        assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == strings
+    assert random.getstate()[1] == tuple(int(x) for x in ref[-1][2])
+
+
+def test_align_many_c3_first_matches_pin():
+    """C3 size, three pipelined alignments: the first equals the oracle pin (tests/golden/c3_aln.json), all three
+    reproduce both inputs at the golden cost, and each later one starts from the state the previous left."""
+    import bench
+    from globalign_amd import _native
+    wl = bench.WORKLOADS["c3"]
+    s1, s2 = bench.workload_pair(wl)
+    tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
+    pin = json.load(open(os.path.join(GOLDEN, "c3_aln.json")))
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(s1), tables.codes(s2), tables)
+        random.seed(0)
+        mt0 = np.array(random.getstate()[1], dtype=np.uint32)
+        runs, mt3 = eng.align_many(mt0, s1, s2, 3)
+        cost0, (a, mid, b), st0 = runs[0]
+        assert st0 == 0 and cost0 == pin["cost"] and len(mid) == pin["aln_len"]
+        assert aln_digest(a, mid, b) == pin["aln_sha16"]
+        for cost, (a, mid, b), st in runs:
+            assert st == 0 and cost == pin["cost"]
+            assert a.replace("-", "") == s1 and b.replace("-", "") == s2
+        # alignment 1 = a single align() from the state alignment 0 left
+        _, _, _, mt1 = eng.align(mt0, s1, s2)
+        c1, strings1, _, mt2 = eng.align(mt1, s1, s2)
+        assert strings1 == runs[1][1]
+        _, strings2, _, mt3b = eng.align(mt2, s1, s2)
+        assert strings2 == runs[2][1] and mt3.tolist() == mt3b.tolist()
+    finally:
+        eng.close()
