@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -340,12 +343,12 @@ struct ga_ctx {
     // pipelined repeated alignments (ga_problem_align_many): two slots of traceback words, walk
     // buffers and events; the walk runs on its own stream beside the next fill
     struct PipeSlot {
-        DevBuf tb, rng, ops, result;
+        DevBuf tb, hand, flags, out_last, rng, ops, result;
         hipEvent_t f0 = nullptr, f1 = nullptr, fdone = nullptr, w0 = nullptr, w1 = nullptr;
         uint32_t* tab_pin = nullptr;  // pinned staging of the walk's table slice
         int64_t tab_cap = 0;
-    } pipe[2];
-    hipStream_t wstream = nullptr;
+    } pipe[3];
+    hipStream_t wstream = nullptr, fstream2 = nullptr;
     int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
     RngTable many_rng;
     bool walk_rng_ready = false;
@@ -502,7 +505,14 @@ struct Band {
     bool band = false;          // fill rows r0+1 .. r0+mb only (the boundary is already computed)
     int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
     int ckpt_rows = 0;
-    DevBuf* tbuf = nullptr;     // traceback words into this buffer instead of ctx->tb (pipelined alignments)
+    // pipelined alignments (align_many): a fill with buffers and a stream of its own, so that two
+    // fills can run at once; the boundary is computed by the first fill only
+    DevBuf* tbuf = nullptr;     // traceback words instead of ctx->tb
+    DevBuf* hbuf = nullptr;     // workgroup hand-off edges instead of ctx->hand
+    DevBuf* fbuf = nullptr;     // ticket / abort words instead of ctx->flags
+    DevBuf* obuf = nullptr;     // H'(m, n) instead of ctx->out_last
+    hipStream_t stream = nullptr;
+    bool skip_boundary = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // fill timing events instead of ctx->ev[0 / 1]
 };
 
@@ -548,21 +558,26 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     }
     // traceback words cover T 64-column stripes per fill stripe
     DevBuf& tbb = bd.tbuf ? *bd.tbuf : c->tb;
+    DevBuf& hb = bd.hbuf ? *bd.hbuf : c->hand;
+    DevBuf& fb = bd.fbuf ? *bd.fbuf : c->flags;
+    DevBuf& ob = bd.obuf ? *bd.obuf : c->out_last;
+    hipStream_t st = bd.stream ? bd.stream : c->stream;
+    HIPCHK(ob.ensure(sizeof(int) * 4));
     if (tb) HIPCHK(tbb.ensure((size_t)c->nstripes * c->T * c->TC * 1024));
-    HIPCHK(c->hand.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
+    HIPCHK(hb.ensure(sizeof(int2) * (size_t)c->nslabs * (m + 1)));
     // workgroup hand-off rows read by a successor start as ga::HAND_SENT (bytes 0x80)
     if (c->nslabs > 1)
-        HIPCHK(hipMemsetAsync(c->hand.p, 0x80, sizeof(int2) * (size_t)(c->nslabs - 1) * (m + 1), c->stream));
-    HIPCHK(c->flags.ensure(sizeof(unsigned) * 16));
+        HIPCHK(hipMemsetAsync(hb.p, 0x80, sizeof(int2) * (size_t)(c->nslabs - 1) * (m + 1), st));
+    HIPCHK(fb.ensure(sizeof(unsigned) * 16));
     if (full) {
         if ((m + 1) * (n + 1) > (int64_t)64 << 20) return fail(GA_E_RANGE, "GA_FILL_FULL is for small problems");
         HIPCHK(c->full.ensure(sizeof(int) * 3 * (m + 1) * (n + 1)));
     }
-    unsigned* fl = c->flags.as<unsigned>();
+    unsigned* fl = fb.as<unsigned>();
     // flags layout: [0] ticket, [1] abort
-    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * 16, c->stream));
-    if (!bd.band)
-        ga::launch_boundary(c->stream, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global,
+    HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * 16, st));
+    if (!bd.band && !bd.skip_boundary)
+        ga::launch_boundary(st, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global,
                             c->gh.as<int>(), c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(),
                             c->top.as<int2>(), c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(),
                             c->meta.as<int>(), c->custom, c->bscr.as<int>());
@@ -581,11 +596,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.left = c->left.as<int2>() + bd.r0;
         p.left_prog = nullptr;
     }
-    p.hand = c->hand.as<int2>();
+    p.hand = hb.as<int2>();
     p.ticket = fl;
     p.abort_word = fl + 1;
     p.tb = tb ? tbb.as<uint8_t>() : nullptr;
-    p.out_last = c->out_last.as<int>();
+    p.out_last = ob.as<int>();
     p.edge_prog = c->slab ? c->prog_dev + 1 : nullptr;  // [1]: halo_out rows
     p.edge_out = c->slab ? c->halo_out_ext : nullptr;
     p.full = full ? c->full.as<int>() : nullptr;
@@ -602,11 +617,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
-    HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], c->stream));
-    if (c->diag) ga::launch_fill_diag(c->stream, p, c->qbytes, full);
-    else ga::launch_fill(c->stream, p, c->CB, c->qbytes, tb, full);
+    HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
+    if (c->diag) ga::launch_fill_diag(st, p, c->qbytes, full);
+    else ga::launch_fill(st, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(bd.ev1 ? bd.ev1 : c->ev[1], c->stream));
+    HIPCHK(hipEventRecord(bd.ev1 ? bd.ev1 : c->ev[1], st));
     c->filled_tb = tb;
     return GA_OK;
 }
@@ -896,11 +911,18 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
 }
 
 // ---------------------------------------------------------------- pipelined repeated alignments
+// `count` alignments of the loaded pair, each from the random state the previous one left.  Three
+// slots of traceback words / hand-off edges / walk buffers; fills alternate between two fill
+// streams, so fill k+1 starts on the CUs fill k leaves idle (C3: one fill holds 196 of 256 CUs)
+// and on those its tail frees, and walk k runs on a third stream beside them.  Walks are serial
+// (alignment k's table slice starts where alignment k-1's dispatches ended); a host thread extends
+// the one continuous tie-break stream ahead of them.
 int pipe_setup(ga_ctx* c) {
     if (!c->wstream) HIPCHK(hipStreamCreateWithPriority(&c->wstream, hipStreamNonBlocking, c->priority));
+    if (!c->fstream2) HIPCHK(hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, c->priority));
     if (!c->pipe_pin) {
         void* hp = nullptr;
-        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 16, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 32, hipHostMallocDefault));
         c->pipe_pin = static_cast<int*>(hp);
     }
     const int64_t per = c->m + c->n + 1;
@@ -922,20 +944,25 @@ int pipe_setup(ga_ctx* c) {
     return GA_OK;
 }
 
-// fill of alignment k into slot k & 1, then its cost inputs into pinned memory, then `fdone`
-int pipe_fill(ga_ctx* c, int slot) {
+// fill of an alignment into slot `slot` on stream `st`, then its cost inputs into pinned memory, then `fdone`
+int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool boundary) {
     auto& sl = c->pipe[slot];
     Band bd;
     bd.tbuf = &sl.tb;
+    bd.hbuf = &sl.hand;
+    bd.fbuf = &sl.flags;
+    bd.obuf = &sl.out_last;
+    bd.stream = st;
+    bd.skip_boundary = !boundary;
     bd.ev0 = sl.f0;
     bd.ev1 = sl.f1;
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
     int* pin = c->pipe_pin + 8 * slot;
-    HIPCHK(hipMemcpyAsync(pin, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(pin + 4, c->meta.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(pin + 5, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(pin + 6, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipEventRecord(sl.fdone, c->stream));
+    HIPCHK(hipMemcpyAsync(pin, sl.out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pin + 4, c->meta.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pin + 5, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pin + 6, sl.flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(sl.fdone, st));
     return GA_OK;
 }
 
@@ -944,54 +971,90 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     const double t0 = now_ms();
     if (int r = pipe_setup(c)) return r;
     const int64_t m = c->m, n = c->n, per = m + n + 1;
-    if (int r = pipe_fill(c, 0)) return r;
-    RngTable& R = c->many_rng;  // one continuous stream for all `count` alignments
-    double rng_ms = 0.0;
-    {
-        const double t1 = now_ms();
-        R.start(mt_state);
-        R.extend(per);
-        rng_ms += now_ms() - t1;
+    hipStream_t fs[2] = {c->stream, c->fstream2};
+    // fill 0 computes the boundary; fill 1 (other stream) starts after it
+    if (int r = pipe_fill(c, 0, fs[0], true)) return r;
+    if (count > 1) {
+        HIPCHK(hipStreamWaitEvent(fs[1], c->pipe[0].f0, 0));
+        if (int r = pipe_fill(c, 1, fs[1], false)) return r;
     }
+    // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
+    // vectors are reserved up front: the walks read earlier entries while later ones are written)
+    RngTable& R = c->many_rng;
+    R.start(mt_state);
+    R.tab.reserve((size_t)count * per);
+    R.step_end.reserve((size_t)count * per + 4);
+    R.acc.reserve((size_t)18 * count * per + 8);
+    const uint32_t* tabp = R.tab.data();  // stable: the capacity is reserved
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t ready = 0;  // entries available to the walks (under mu)
+    double rng_ms = 0.0;
+    std::thread producer([&] {
+        for (int k = 0; k < count; k++) {
+            const double t1 = now_ms();
+            R.extend((int64_t)(k + 1) * per);
+            rng_ms += now_ms() - t1;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                ready = (int64_t)(k + 1) * per;
+            }
+            cv.notify_all();
+        }
+    });
+    int rc = GA_OK;
     int64_t G = 0;  // global dispatches consumed by the alignments before k
     float fill_sum = 0.f, walk_sum = 0.f;
-    for (int k = 0; k < count; k++) {
-        auto& sl = c->pipe[k & 1];
+    for (int k = 0; k < count && rc == GA_OK; k++) {
+        auto& sl = c->pipe[k % 3];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return ready >= G + per; });
+        }
         // walk k: after fill k, on the walk stream, over its table slice [G, G + per)
-        HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
-        std::memcpy(sl.tab_pin, R.tab.data() + G, sizeof(uint32_t) * per);
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
                           c->wstream, sl.w0, sl.w1};
-        if (int r = run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb)) return r;
-        // fill k+1 into the other slot (after walk k-1, which read it), beside walk k
-        if (k + 1 < count) {
-            auto& nx = c->pipe[(k + 1) & 1];
-            if (k >= 1) HIPCHK(hipStreamWaitEvent(c->stream, nx.w1, 0));
-            if (int r = pipe_fill(c, (k + 1) & 1)) return r;
-            // the table for alignment k+1: G_{k+1} <= G + per, so entries up to G + 2 per
-            const double t1 = now_ms();
-            R.extend(G + 2 * per);
-            rng_ms += now_ms() - t1;
-        }
-        // alignment k's cost and strings
-        HIPCHK(hipEventSynchronize(sl.fdone));
-        const int* pin = c->pipe_pin + 8 * (k & 1);
-        if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
-        cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
-        float f = 0.f;
-        if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
-        WalkStart st{m, n, 0, 0, 0, 1};
-        int reason = 0;
-        int64_t len = 0;
-        char* a_k = oa + (size_t)k * cap;
-        char* m_k = om + (size_t)k * cap;
-        char* b_k = ob + (size_t)k * cap;
-        if (int r = walk_segment(c, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, &wb)) return r;
-        walk_sum += c->walk_ms;
-        if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
-                                  &tb_status[k]))
-            return r;
-        G += st.D;
+        auto step = [&]() -> int {
+            HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
+            std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
+            if (int r = run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb)) return r;
+            // fill k+2: on fill k's stream (it starts when fill k ends, beside fill k+1), into the slot
+            // walk k-1 has read
+            if (k + 2 < count) {
+                auto& nx = c->pipe[(k + 2) % 3];
+                hipStream_t st = fs[k & 1];
+                if (k >= 1) HIPCHK(hipStreamWaitEvent(st, nx.w1, 0));
+                if (int r = pipe_fill(c, (k + 2) % 3, st, false)) return r;
+            }
+            // alignment k's cost and strings
+            HIPCHK(hipEventSynchronize(sl.fdone));
+            const int* pin = c->pipe_pin + 8 * (k % 3);
+            if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+            cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
+            float f = 0.f;
+            if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
+            WalkStart st{m, n, 0, 0, 0, 1};
+            int reason = 0;
+            int64_t len = 0;
+            char* a_k = oa + (size_t)k * cap;
+            char* m_k = om + (size_t)k * cap;
+            char* b_k = ob + (size_t)k * cap;
+            if (int r = walk_segment(c, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, &wb)) return r;
+            walk_sum += c->walk_ms;
+            if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
+                                      &tb_status[k]))
+                return r;
+            G += st.D;
+            return GA_OK;
+        };
+        rc = step();
+    }
+    producer.join();
+    if (rc != GA_OK) {
+        (void)hipStreamSynchronize(fs[0]);
+        (void)hipStreamSynchronize(fs[1]);
+        (void)hipStreamSynchronize(c->wstream);
+        return rc;
     }
     state_after(R, G, mt_state);  // the state the last alignment leaves (random.getstate() layout)
     c->fill_ms = fill_sum / count;
@@ -1075,13 +1138,14 @@ void ga_ctx_destroy(ga_ctx* c) {
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& sl : c->pipe) {
-        for (DevBuf* b : {&sl.tb, &sl.rng, &sl.ops, &sl.result}) b->release();
+        for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result}) b->release();
         for (hipEvent_t e : {sl.f0, sl.f1, sl.fdone, sl.w0, sl.w1})
             if (e) (void)hipEventDestroy(e);
         if (sl.tab_pin) (void)hipHostFree(sl.tab_pin);
     }
     if (c->pipe_pin) (void)hipHostFree(c->pipe_pin);
     if (c->wstream) (void)hipStreamDestroy(c->wstream);
+    if (c->fstream2) (void)hipStreamDestroy(c->fstream2);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_dep) (void)hipEventDestroy(c->ev_dep);
@@ -1165,7 +1229,9 @@ int ga_problem_align_many(ga_ctx* c, int32_t count, uint32_t* mt_state, const ch
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status || !cost_out)
         return fail(GA_E_ARG, "null argument");
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
-    if (count == 1 || band_rows(c) > 0) {
+    // three slots of traceback words: beyond 96 GB of them, one alignment after another
+    const bool fits = (int64_t)3 * ((c->n + 63) / 64) * 64 * c->m * c->CB <= ((int64_t)96 << 30);
+    if (count == 1 || band_rows(c) > 0 || !fits) {
         // one alignment, or banded tracebacks (whose band fills hold every CU): one after another
         const double t0 = now_ms();
         float fs = 0.f, ws = 0.f, rs = 0.f;
@@ -1354,6 +1420,19 @@ int ga_debug_rng(const uint32_t* state, int64_t steps, uint32_t* tab_out, int64_
     const double t0 = now_ms();
     build_rng(state, steps, R);
     if (ms_out) *ms_out = now_ms() - t0;
+    std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
+    state_after(R, D, state_out);
+    return GA_OK;
+}
+
+// CPU-only check of the resumable table stream (tests): entries for `steps` dispatches built in
+// `chunk`-sized extensions, and the state after the first D of them.
+int ga_debug_rng_chunked(const uint32_t* state, int64_t steps, int64_t chunk, uint32_t* tab_out, int64_t D,
+                         uint32_t* state_out) {
+    if (!state || !tab_out || !state_out || D < 0 || D > steps || chunk < 1) return fail(GA_E_ARG, "bad argument");
+    RngTable R;
+    R.start(state);
+    for (int64_t b = chunk; b < steps + chunk; b += chunk) R.extend(std::min(b, steps));
     std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
     state_after(R, D, state_out);
     return GA_OK;

@@ -61,3 +61,27 @@ def test_tiebreak_table_matches_cpython(lib, seed, steps):
         assert lib.ga_debug_rng(st.ctypes.data, steps, tab.ctypes.data, D, out.ctypes.data, C.byref(ms)) == 0
         assert tab.tolist() == want
         assert state_digest((3, tuple(int(x) for x in out), None)) == state_digest(states[D])
+
+
+@pytest.mark.parametrize("seed,steps,chunk", [(2, 5000, 1), (5, 20000, 777), (9, 12000, 4000), (4, 3001, 3001)])
+def test_tiebreak_stream_resumes_exactly(lib, seed, steps, chunk):
+    """The resumable table stream (align_many's continuous tie-break table): built in chunks it equals the
+    one-shot table, and its entries from any dispatch G on equal a fresh table started from the state
+    after G dispatches (consecutive alignments share one stream)."""
+    lib.ga_debug_rng.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+    lib.ga_debug_rng_chunked.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p]
+    random.seed(seed)
+    st = np.array(random.getstate()[1], dtype=np.uint32)
+    one = np.zeros(steps, np.uint32)
+    s1 = np.zeros(625, np.uint32)
+    ms = C.c_double(0)
+    assert lib.ga_debug_rng(st.ctypes.data, steps, one.ctypes.data, steps, s1.ctypes.data, C.byref(ms)) == 0
+    ch = np.zeros(steps, np.uint32)
+    s2 = np.zeros(625, np.uint32)
+    G = steps // 3
+    assert lib.ga_debug_rng_chunked(st.ctypes.data, steps, chunk, ch.ctypes.data, G, s2.ctypes.data) == 0
+    assert ch.tolist() == one.tolist()
+    fresh = np.zeros(steps - G, np.uint32)
+    s3 = np.zeros(625, np.uint32)
+    assert lib.ga_debug_rng(s2.ctypes.data, steps - G, fresh.ctypes.data, 0, s3.ctypes.data, C.byref(ms)) == 0
+    assert fresh.tolist() == one[G:].tolist()
