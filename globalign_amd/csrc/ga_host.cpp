@@ -72,20 +72,17 @@ constexpr int MTN = 624, MTM = 397;
 struct PyMT {
     uint32_t mt[MTN];
     int mti;
+    // one MT19937 twist, branch-free and in three runs without loop-carried dependences the
+    // compiler cannot vectorise (kk+1 is read before it is written; kk-227 was written long before)
+    static inline uint32_t tw(uint32_t a, uint32_t b, uint32_t c) {
+        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+    }
     void twist() {
-        static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
-        int kk = 0;
-        uint32_t y;
-        for (; kk < MTN - MTM; kk++) {
-            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + MTM] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        for (; kk < MTN - 1; kk++) {
-            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + (MTM - MTN)] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        y = (mt[MTN - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
-        mt[MTN - 1] = mt[MTM - 1] ^ (y >> 1) ^ mag01[y & 1u];
+        uint32_t* __restrict m = mt;
+        for (int kk = 0; kk < MTN - MTM; kk++) m[kk] = tw(m[kk], m[kk + 1], m[kk + MTM]);
+        for (int kk = MTN - MTM; kk < MTN - 1; kk++) m[kk] = tw(m[kk], m[kk + 1], m[kk + (MTM - MTN)]);
+        m[MTN - 1] = tw(m[MTN - 1], m[0], m[MTM - 1]);
         mti = 0;
     }
     inline uint32_t next() {
@@ -735,12 +732,24 @@ inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 
 // Wait for the walk; decode the levels of dispatches [st.D, D_end) into alignment columns in walk
 // order starting at (st.i, st.j) (global columns).  Returns the end state through `st` and `reason`.
+int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const char* a_chr, const char* b_chr,
+                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced);
+
 int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const char* b_chr, char* oa, char* om,
                  char* ob, int64_t cap, int64_t& len, const WalkBufs* wbp = nullptr) {
     const WalkBufs wb = wbp ? *wbp : ctx_walk_bufs(c);
     int res[16];
     HIPCHK(hipMemcpyAsync(res, wb.result, sizeof(int) * 16, hipMemcpyDeviceToHost, wb.stream));
     HIPCHK(hipStreamSynchronize(wb.stream));
+    return decode_segment(c, res, st, reason, a_chr, b_chr, oa, om, ob, cap, len, wb, false);
+}
+
+// The alignment columns of a finished walk (its result words already read): levels of dispatches
+// [st.D, res[0]) decoded in walk order starting at (st.i, st.j).  synced: the walk is known to be
+// complete, so its levels are read with a plain copy instead of on its stream (which may already
+// hold the next walk).
+int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const char* a_chr, const char* b_chr,
+                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced) {
     c->walk_waits = res[4];
     c->walk_tiles = res[5];
     c->walk_t_tile = res[6];
@@ -749,15 +758,20 @@ int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const
     c->walk_c_total = res[9];
     c->walk_load_ticks = res[10];
     c->walk_load_count = res[11];
-    HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
+    if (!synced) HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
     const int64_t D0 = st.D, D1 = res[0];
     reason = res[3];
     // levels are packed 2 bits per dispatch, dispatch k at bits 30 - 2*(k & 15) of u32 word k >> 4
     const int64_t w0 = D0 >> 4, w1 = (D1 + 15) >> 4;
     std::vector<uint32_t> ops((size_t)std::max<int64_t>(w1 - w0, 0));
-    if (D1 > D0)
-        HIPCHK(hipMemcpyAsync(ops.data(), wb.ops + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, wb.stream));
-    HIPCHK(hipStreamSynchronize(wb.stream));
+    if (synced) {
+        if (D1 > D0) HIPCHK(hipMemcpy(ops.data(), wb.ops + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    } else {
+        if (D1 > D0)
+            HIPCHK(hipMemcpyAsync(ops.data(), wb.ops + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  wb.stream));
+        HIPCHK(hipStreamSynchronize(wb.stream));
+    }
     const int64_t m = c->m, n = c->n_global;
     int64_t i = st.i, j = st.j;
     int L = st.L;
@@ -972,11 +986,11 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     if (int r = pipe_setup(c)) return r;
     const int64_t m = c->m, n = c->n, per = m + n + 1;
     hipStream_t fs[2] = {c->stream, c->fstream2};
-    // fill 0 computes the boundary; fill 1 (other stream) starts after it
+    // fill 0 computes the boundary; fills 1 (other stream) and 2 (after fill 0) start after it
     if (int r = pipe_fill(c, 0, fs[0], true)) return r;
-    if (count > 1) {
-        HIPCHK(hipStreamWaitEvent(fs[1], c->pipe[0].f0, 0));
-        if (int r = pipe_fill(c, 1, fs[1], false)) return r;
+    for (int k = 1; k < std::min(count, 3); k++) {
+        if (k == 1) HIPCHK(hipStreamWaitEvent(fs[1], c->pipe[0].f0, 0));
+        if (int r = pipe_fill(c, k, fs[k & 1], false)) return r;
     }
     // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
     // vectors are reserved up front: the walks read earlier entries while later ones are written)
@@ -988,59 +1002,89 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     const uint32_t* tabp = R.tab.data();  // stable: the capacity is reserved
     std::mutex mu;
     std::condition_variable cv;
-    int64_t ready = 0;  // entries available to the walks (under mu)
+    int64_t ready = 0;         // entries available to the walks (under mu)
+    int64_t target = per;      // entries the producer builds up to (under mu)
+    bool quit = false;
     double rng_ms = 0.0;
     std::thread producer([&] {
-        for (int k = 0; k < count; k++) {
+        for (;;) {
+            int64_t want;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return quit || target > ready; });
+                if (quit) return;
+                want = std::min<int64_t>(target, (int64_t)count * per);
+                if (want <= ready) {
+                    target = ready;  // nothing more can be built
+                    continue;
+                }
+            }
             const double t1 = now_ms();
-            R.extend((int64_t)(k + 1) * per);
+            R.extend(want);
             rng_ms += now_ms() - t1;
             {
                 std::lock_guard<std::mutex> lk(mu);
-                ready = (int64_t)(k + 1) * per;
+                ready = want;
             }
             cv.notify_all();
         }
     });
-    int rc = GA_OK;
-    int64_t G = 0;  // global dispatches consumed by the alignments before k
-    float fill_sum = 0.f, walk_sum = 0.f;
-    for (int k = 0; k < count && rc == GA_OK; k++) {
+    // walk k over its table slice [G, G + per), after fill k, on the walk stream
+    auto start_walk = [&](int k, int64_t G) -> int {
         auto& sl = c->pipe[k % 3];
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return ready >= G + per; });
         }
-        // walk k: after fill k, on the walk stream, over its table slice [G, G + per)
+        HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
+        std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
+        const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
+                          c->wstream, sl.w0, sl.w1};
+        return run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb);
+    };
+    int rc = start_walk(0, 0);
+    int64_t G = 0;  // global dispatches consumed by the alignments before k
+    int64_t Dmax = 0;
+    float fill_sum = 0.f, walk_sum = 0.f;
+    for (int k = 0; k < count && rc == GA_OK; k++) {
+        auto& sl = c->pipe[k % 3];
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
                           c->wstream, sl.w0, sl.w1};
         auto step = [&]() -> int {
-            HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
-            std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
-            if (int r = run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb)) return r;
-            // fill k+2: on fill k's stream (it starts when fill k ends, beside fill k+1), into the slot
-            // walk k-1 has read
-            if (k + 2 < count) {
-                auto& nx = c->pipe[(k + 2) % 3];
-                hipStream_t st = fs[k & 1];
-                if (k >= 1) HIPCHK(hipStreamWaitEvent(st, nx.w1, 0));
-                if (int r = pipe_fill(c, (k + 2) % 3, st, false)) return r;
+            // walk k done: its dispatch count fixes where walk k+1's table slice starts
+            HIPCHK(hipEventSynchronize(sl.w1));
+            int res[16];
+            HIPCHK(hipMemcpy(res, sl.result.p, sizeof(int) * 16, hipMemcpyDeviceToHost));
+            const int64_t Dk = res[0];
+            Dmax = std::max(Dmax, Dk);
+            {
+                // keep the producer an alignment's worth (and some) ahead of the next walk
+                std::lock_guard<std::mutex> lk(mu);
+                target = std::max(target, G + Dk + per + Dmax + Dmax / 8);
             }
-            // alignment k's cost and strings
-            HIPCHK(hipEventSynchronize(sl.fdone));
+            cv.notify_all();
+            if (k + 1 < count)
+                if (int r = start_walk(k + 1, G + Dk)) return r;
+            // alignment k's cost (fill k finished before walk k started) and walk time, before slot k's
+            // pinned words and events are reused
             const int* pin = c->pipe_pin + 8 * (k % 3);
             if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
             cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
             float f = 0.f;
             if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
+            float wms = 0.f;
+            if (hipEventElapsedTime(&wms, sl.w0, sl.w1) == hipSuccess) walk_sum += wms;
+            // fill k+3 into slot k's buffers (walk k has read them), after fill k+1 on its stream
+            if (k + 3 < count)
+                if (int r = pipe_fill(c, k % 3, fs[(k + 1) & 1], false)) return r;
+            // alignment k's strings, while walk k+1 and the fills run
             WalkStart st{m, n, 0, 0, 0, 1};
             int reason = 0;
             int64_t len = 0;
             char* a_k = oa + (size_t)k * cap;
             char* m_k = om + (size_t)k * cap;
             char* b_k = ob + (size_t)k * cap;
-            if (int r = walk_segment(c, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, &wb)) return r;
-            walk_sum += c->walk_ms;
+            if (int r = decode_segment(c, res, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, wb, true)) return r;
             if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
                                       &tb_status[k]))
                 return r;
@@ -1049,6 +1093,11 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         };
         rc = step();
     }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        quit = true;
+    }
+    cv.notify_all();
     producer.join();
     if (rc != GA_OK) {
         (void)hipStreamSynchronize(fs[0]);
