@@ -319,7 +319,9 @@ struct ga_ctx {
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
     int T = 1, T_req = 0, nwc_req = 0;
-    int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal (GA_FILL_MODE)
+    int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal, 3 lane-skewed (GA_FILL_MODE)
+    int lane_T_req = 0;        // columns per lane of the lane-skewed kernel (GA_LANE_COLS_PER_LANE; 0: automatic)
+    bool lane = false;         // the last enqueued fill used the lane-skewed kernel
     int diag_T_req = 0;        // columns per lane of the anti-diagonal kernel (GA_DIAG_COLS_PER_LANE; 0: automatic)
     bool diag = false;         // the last enqueued fill used the anti-diagonal kernel      // columns per lane of the fill (T_req 0: automatic; GA_COLS_PER_LANE)
     int64_t GV_m = 0, GH_n = 0;
@@ -393,6 +395,47 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full, int64_t ncols = -1) {
     c->nstripes = (int)((ncol + 64 * T - 1) / (64 * T));
     c->nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : c->nstripes <= 4 * c->num_cu ? 4 : 8;
     c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
+}
+
+// Lane-skewed fill geometry: TD columns per lane, NWC compute waves per workgroup,
+// every stripe resident at once (a stripe waits on its left neighbour only, so the whole chain must
+// run concurrently).  The cost model is the measured step of tools/micro/lane_bench.hip (cycles per
+// step per wave at one / two waves per SIMD, with the kernel's per-step LDS traffic and the DPP
+// shift-register output) times the chain's length, m steps plus ~74 steps of skew per stripe.
+// Returns false (row scan) when the profile table does not fit beside the rings.
+bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out) {
+    if (c->qbytes != 1 || c->K > 32 || c->CB < 1) return false;
+    static const double cyc[4][2] = {{61, 105}, {89, 160}, {131, 245}, {226, 423}};  // TD = 1, 2, 4, 8
+    const int64_t cus = c->num_cu;
+    int bestT = 0, bestN = 0;
+    double best = 0;
+    for (int ti = 0; ti < 4; ti++) {
+        const int T = 1 << ti;
+        if (c->lane_T_req && c->lane_T_req != T) continue;
+        // a slab with a right neighbour hands column n on: its last stripe must be whole
+        if (c->col0 + c->n < c->n_global && ncol % (64 * T) != 0) continue;
+        const int64_t ns = (ncol + 64 * T - 1) / (64 * T);
+        const int nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : ns <= 4 * cus ? 4 : 8;
+        if (ns > nwc * cus) continue;  // not every stripe resident
+        const int wps = (ns + 4 * cus - 1) / (4 * cus) > 1 ? 1 : 0;
+        const double t = ((double)c->m + 74.0 * (double)ns) * cyc[ti][wps];
+        if (!bestT || t < best) {
+            best = t;
+            bestT = T;
+            bestN = nwc;
+        }
+    }
+    if (!bestT) return false;
+    const size_t budget = 150 * 1024;
+    int qr = 4096;
+    while (qr > 256 && ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget) qr >>= 1;
+    if (ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget || qr < bestN * 64 + 192) return false;
+    c->T = bestT;
+    c->nwc = bestN;
+    c->nstripes = (int)((ncol + 64 * bestT - 1) / (64 * bestT));
+    c->nslabs = (c->nstripes + c->nwc - 1) / c->nwc;
+    *qrows_out = qr;
+    return true;
 }
 
 int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
@@ -526,6 +569,13 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // (its query-profile ring deeper than a workgroup's skew: NWC stripes x 64*TD steps)
     int qrows = c->qrows;
     c->diag = false;
+    c->lane = false;
+    // score only: the lane-skewed kernel when its chain's skew (~74 steps per stripe)
+    // is short against the m rows every stripe walks (measured: 1M x 125k 60 ms against 107 for the row
+    // scan, C4 244 against 312; 100k x 100k, whose 782 stripes add 58k steps of skew, 13.5 against 12.6)
+    if (!tb && !bd.band && bd.ckpt == nullptr && (c->diag_req == 3 || c->diag_req == 0) && lane_geometry(c, n, &qrows) &&
+        (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
+        c->lane = true;
     // automatic: score-only fills of tall problems on one GPU (m >= 4 n, <= 8 stripes per CU).
     // Measured (profiles/r01/diag_sweep.txt): 1M x 125k 80 ms (TD = 1) against 107 ms for the row
     // scan, 1M x 250k 126 ms (TD = 2) against 141 ms; the row scan wins on square shapes (C4 313 ms
@@ -535,7 +585,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     const int auto_td = (n + 63) / 64 <= 8 * (int64_t)c->num_cu ? 1 : 2;
     const bool auto_diag = c->diag_req == 0 && !tb && !bd.band && !c->slab && m >= 4 * n &&
                            (n + 64 * auto_td - 1) / (64 * auto_td) <= 8 * (int64_t)c->num_cu;
-    if ((!tb || (full && c->qbytes == 1)) && (c->diag_req == 2 || auto_diag) && bd.ckpt == nullptr) {
+    if (!c->lane && (!tb || (full && c->qbytes == 1)) && (c->diag_req == 2 || auto_diag) && bd.ckpt == nullptr) {
         int td = full ? std::min(std::max(c->diag_T_req, 1), 2)
                       : c->diag_T_req == 1 || c->diag_T_req == 2 || c->diag_T_req == 4 ? c->diag_T_req
                       : auto_diag ? auto_td : 1;
@@ -549,7 +599,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         while (qrows > 128 && (size_t)c->K * (qrows + 16) * c->qbytes > 64 * 1024) qrows >>= 1;
         c->diag = qrows >= c->nwc * (64 * c->T + 16) + 64 * c->T + 64;
     }
-    if (!c->diag) {
+    if (!c->diag && !c->lane) {
         qrows = c->qrows;
         set_stripes(c, c->T_req, tb, full, n);
     }
@@ -615,7 +665,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
-    if (c->diag) ga::launch_fill_diag(st, p, c->qbytes, full);
+    if (c->lane) ga::launch_fill_lane(st, p);
+    else if (c->diag) ga::launch_fill_diag(st, p, c->qbytes, full);
     else ga::launch_fill(st, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(bd.ev1 ? bd.ev1 : c->ev[1], st));
@@ -1144,7 +1195,9 @@ int ga_ctx_create(int device, ga_ctx** out) {
             c->num_cu = cus;
         if (const char* e = getenv("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
         if (const char* e = getenv("GA_FILL_NWC")) c->nwc_req = atoi(e);
-        if (const char* e = getenv("GA_FILL_MODE")) c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : 0;
+        if (const char* e = getenv("GA_FILL_MODE"))
+            c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : !strcmp(e, "lane") ? 3 : 0;
+        if (const char* e = getenv("GA_LANE_COLS_PER_LANE")) c->lane_T_req = atoi(e);
         if (const char* e = getenv("GA_DIAG_COLS_PER_LANE")) c->diag_T_req = atoi(e);
     }
     // The fill runs on a stream of the greatest priority.  HIP keeps a separate pool of hardware
@@ -1457,6 +1510,18 @@ int ga_debug_geometry(ga_ctx* c, int32_t* out4) {
     out4[1] = c->nstripes;
     out4[2] = c->nwc;
     out4[3] = c->nslabs;
+    return GA_OK;
+}
+
+// Diagnostics: the kernel of the last enqueued fill (0 row scan, 1 per-column anti-diagonal, 2 lane-skewed)
+// and its geometry {T, nstripes, nwc, nslabs}.
+int ga_debug_fill_kind(ga_ctx* c, int32_t* out5) {
+    if (!c || !out5) return fail(GA_E_ARG, "null argument");
+    out5[0] = c->lane ? 2 : c->diag ? 1 : 0;
+    out5[1] = c->T;
+    out5[2] = c->nstripes;
+    out5[3] = c->nwc;
+    out5[4] = c->nslabs;
     return GA_OK;
 }
 

@@ -1,0 +1,423 @@
+// ga_lane.hip -- the lane-skewed anti-diagonal score fill (dp_array_forward, globaligner.py:366-392;
+// get_next_best_costs :317-363), score only.  DESIGN.md 5.6.
+//
+// A stripe is 64*TD columns; lane l owns the TD adjacent columns j0+l*TD+1 .. j0+l*TD+TD and at step
+// t works on row i = t - l + 1 of all of them.  So a lane's TD columns are one in-register row
+// segment (h1' chained through them, 5 VALU per cell) and only the lane-to-lane hand-over is skewed:
+// lane l takes h1'(i, left) from lane l-1's step t-1 and H'(i-1, left) from its step t-2 through
+// two DPP lane shifts per step.  Compared with the per-column skew of fill_diag_kernel the skew
+// across a stripe is 64 steps instead of 64*TD, and compared with the row scan (fill_kernel) no
+// step pays a 64-lane scan: tools/micro/lane_bench.hip puts the TD = 8 step at 0.41 SIMD cycles
+// per cell with every per-step overhead of this kernel (the blocked row scan runs C4 at 0.77).
+//
+// Per 8-step sub-chunk a compute wave
+//   * reads the next sub-chunk's 8 left-edge rows (H', h1') from its input ring (LDS, broadcast),
+//   * reads its lanes' profile windows: sub' bytes of 8 consecutive rows per column from a table
+//     whose dword r holds rows r..r+3 of one code (any start row is dword aligned), so a step's
+//     profile value is an SDWA byte select folded into M' = H'(diag) + sub',
+//   * writes lane 63's 8 outputs: each step shifts lane 63's (H', h1') into a DPP shift register
+//     (wave_shl:1), whose lanes 56..63 then hold the sub-chunk's rows; one 8-lane store.
+// The IO wave feeds ring 0 from HBM (the slab's left edge, the previous workgroup's hand-off rows
+// or another GPU's halo), drains the last wave's ring to HBM and fills the profile table, exactly
+// as the row-scan and per-column anti-diagonal kernels do (ga_kernels.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "ga_device.h"
+#include "ga_sync.h"
+
+namespace ga {
+
+// LDS counters of the lane kernel (dwords of the 256-byte counter block): cons(k) = rows of ring k
+// its reader no longer needs at [2k], prod(k) = rows of ring k written at [2k-1] (k >= 1) and
+// [LK_PROD0] (ring 0, the IO wave's), so compute wave w publishes {cons(w), prod(w+1)} in one store
+enum { LK_PROD0 = 31, LK_PRODQ = 40, LK_ABORT = 41, LK_SLAB = 42 };
+constexpr int LK_CNT_BYTES = 256;
+constexpr int LK_SUB = 8;      // steps per sub-chunk
+constexpr int LK_QMIRROR = 8;  // profile slots mirrored past the ring's end (a window reads idx .. idx+4)
+constexpr unsigned LK_DONE = 0x7fffffffu;
+typedef unsigned lk_v2u __attribute__((ext_vector_type(2)));
+
+size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
+    return (size_t)LK_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + LK_QMIRROR) * 4 +
+           (size_t)K * 32;  // + the K x K int8 sub' table (K <= 32)
+}
+
+// one step of the fast path; U: the step's byte in the profile dwords
+template <int TD, int U>
+__device__ __forceinline__ void lane_step(int (&H)[TD], int (&Y)[TD], int& Xl, int& Hl, int& HLp, int& RH, int& RX,
+                                          int eh, int ex, const uint32_t (&q)[TD], int o) {
+    int X = __builtin_amdgcn_update_dpp(ex, Xl, 0x138, 0xf, 0xf, false);          // h1'(i, left): lane 0 the edge
+    const int HLn = __builtin_amdgcn_update_dpp(eh, Hl, 0x138, 0xf, 0xf, false);  // H'(i, left), the next diagonal
+    int Hd = HLp;
+#pragma unroll
+    for (int k = 0; k < TD; k++) {
+        const int M = Hd + (int)(int8_t)(q[k] >> (8 * U));
+        const int Hn = min(min(M, X), Y[k]);
+        const int Ho = Hn + o;
+        X = min(X, Ho);
+        Y[k] = min(Y[k], Ho);
+        Hd = H[k];
+        H[k] = Hn;
+    }
+    Xl = X;
+    Hl = H[TD - 1];
+    HLp = HLn;
+    RH = __builtin_amdgcn_update_dpp(Hl, RH, 0x130, 0xf, 0xf, false);  // lane 63 shifts its output in
+    RX = __builtin_amdgcn_update_dpp(Xl, RX, 0x130, 0xf, 0xf, false);
+}
+
+// the masked step of the first sub-chunks (lanes above row 1 keep their row-0 state) and of the
+// sub-chunk in which a partial stripe's column n reaches row m (captured into Hm)
+template <int TD, int U>
+__device__ __forceinline__ void lane_step_masked(int (&H)[TD], int (&Y)[TD], int& Xl, int& Hl, int& HLp, int& RH,
+                                                 int& RX, int eh, int ex, const uint32_t (&q)[TD], int o, int row,
+                                                 bool cap, int ck, int& Hm) {
+    int X = __builtin_amdgcn_update_dpp(ex, Xl, 0x138, 0xf, 0xf, false);
+    const int HLn = __builtin_amdgcn_update_dpp(eh, Hl, 0x138, 0xf, 0xf, false);
+    const bool act = row >= 1;
+    int Hd = HLp;
+#pragma unroll
+    for (int k = 0; k < TD; k++) {
+        const int M = Hd + (int)(int8_t)(q[k] >> (8 * U));
+        const int Hn = min(min(M, X), Y[k]);
+        const int Ho = Hn + o;
+        X = min(X, Ho);
+        if (cap && k == ck) Hm = Hn;
+        Y[k] = act ? min(Y[k], Ho) : Y[k];
+        Hd = H[k];
+        H[k] = act ? Hn : H[k];
+    }
+    Xl = X;
+    Hl = H[TD - 1];
+    HLp = HLn;
+    RH = __builtin_amdgcn_update_dpp(Hl, RH, 0x130, 0xf, 0xf, false);
+    RX = __builtin_amdgcn_update_dpp(Xl, RX, 0x130, 0xf, 0xf, false);
+}
+
+// DBG: per stripe {start, end (s_memrealtime), cycles waiting for edges / profile / ring space,
+// total cycles, HW_ID} into p.dbg (tools/lane_stamps.py)
+template <int NWC, int TD, bool DBG>
+__global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    unsigned* cnt = reinterpret_cast<unsigned*>(smem);
+    int2* ring = reinterpret_cast<int2*>(smem + LK_CNT_BYTES);
+    uint32_t* pq = reinterpret_cast<uint32_t*>(ring + (NWC + 1) * RING);
+    const int QR = p.qrows;  // profile ring rows (power of two)
+    const int QS = QR + LK_QMIRROR;
+    const unsigned qmask = (unsigned)QR - 1u;
+    const int K = p.K;
+    int8_t* stab = reinterpret_cast<int8_t*>(pq + (size_t)K * QS);  // [K][32]: sub'(x, c) at x*32 + c
+    unsigned* abort_sh = cnt + LK_ABORT;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    for (int q = threadIdx.x; q < K * K; q += blockDim.x) stab[(q / K) * 32 + q % K] = (int8_t)p.subp[q];
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[LK_SLAB] = atomicAdd(p.ticket, 1u);
+    __syncthreads();
+    const int g = __builtin_amdgcn_readfirstlane((int)cnt[LK_SLAB]);
+    const int m = p.m, o = p.o;
+    const int nsteps = m + 63;  // lane 63 reaches row m at step m + 62
+    const int nsub = (nsteps + LK_SUB - 1) / LK_SUB;
+    const int nlive = min(NWC, p.nstripes - g * NWC);
+
+    if (w == NWC) {
+        // ---------------- IO wave: edges HBM <-> LDS rings, the profile table ----------------
+        const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
+        const unsigned* src_prog = g == 0 ? p.left_prog : nullptr;
+        const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
+        const bool src_sc1 = p.left_prog != nullptr;
+        const bool last_slab = g == p.nslabs - 1;
+        int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
+        int2* rin0 = ring;
+        const int2* rout = ring + nlive * RING;
+        const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
+        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
+        // dword row r of code c: sub'(a_r .. a_r+3, c), rows outside 1..m zero.  A lane's window
+        // may start up to 3 rows above row 1 (its first sub-chunk), so rows -2..0 are written too.
+        auto put_dword = [&](int r) {
+            int x[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                ok[u] = r + u >= 1 && r + u <= m;
+                x[u] = ok[u] ? p.a[r + u - 1] : 0;
+            }
+            const unsigned slot = (unsigned)(r - 1) & qmask;
+            for (int c = 0; c < K; c++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) v |= ok[u] ? (uint32_t)(uint8_t)stab[x[u] * 32 + c] << (8 * u) : 0u;
+                pq[c * QS + slot] = v;
+                if (slot < (unsigned)LK_QMIRROR) pq[c * QS + QR + slot] = v;
+            }
+        };
+        if (lane < 3) put_dword(lane - 2);
+        while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
+            bool moved = false;
+            if (q_next < (unsigned)m) {
+                // the slowest wave reads rows above (its output rows) - 16, so slots of rows below
+                // that + QR are free
+                const unsigned pl = lds_ld(&cnt[2 * nlive - 1]);
+                const unsigned space = (pl > 32u ? pl - 32u : 0u) + (unsigned)QR;
+                const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
+                if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
+                    const unsigned r = q_next + 1 + lane;
+                    if (r <= hi) put_dword((int)r);
+                    if (lane == 0) lds_st(&cnt[LK_PRODQ], hi == (unsigned)m ? LK_DONE : hi);
+                    q_next = hi;
+                    moved = true;
+                }
+            }
+            if (in_next < (unsigned)m && in_sent) {
+                const unsigned cap = min(min(lds_ld(&cnt[0]) + RING, (unsigned)m), in_next + in_win);
+                if (cap > in_next) {
+                    const unsigned r = in_next + 1 + lane;
+                    const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
+                    const unsigned long long ok = __ballot(e1.x != HAND_SENT);
+                    const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;
+                    // poll window: a reader waiting on the writer looks at the next 32 rows (one
+                    // sc1 round trip is ~1 us, and the chain produces a row every ~40-180 ns)
+                    in_win = k >= cap - in_next ? 64u : 32u;
+                    if (k > 0) {
+                        if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
+                        const unsigned hi = in_next + k;
+                        if (lane == 0) lds_st(&cnt[LK_PROD0], hi == (unsigned)m ? LK_DONE : hi);
+                        in_next = hi;
+                        moved = true;
+                    }
+                }
+            } else if (in_next < (unsigned)m) {
+                const unsigned space = lds_ld(&cnt[0]) + RING;
+                const unsigned avail = src_prog ? min(s_ld(src_prog), (unsigned)m) : (unsigned)m;
+                const unsigned hi = min(min(space, avail), in_next + 64);
+                if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
+                    const unsigned r = in_next + 1 + lane;
+                    if (r <= hi) rin0[(r - 1) & RMASK] = src_sc1 ? unpack64(s_ld64(src + r)) : src[r];
+                    if (lane == 0) lds_st(&cnt[LK_PROD0], hi == (unsigned)m ? LK_DONE : hi);
+                    in_next = hi;
+                    moved = true;
+                }
+            }
+            if (out_next < (unsigned)m) {
+                const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
+                const unsigned hi = min(min(P, (unsigned)m), out_next + 64);
+                if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
+                    const unsigned r = out_next + 1 + lane;
+                    if (r <= hi) {
+                        const int2 e = rout[(r - 1) & RMASK];
+                        if (out_sent) g_st64(dst + r, e);
+                        else s_st64(dst + r, e);  // another GPU's halo
+                        if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
+                    }
+                    if (!out_sent) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) __hip_atomic_store(p.edge_prog, hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    if (lane == 0) lds_st(&cnt[2 * nlive], hi);
+                    out_next = hi;
+                    moved = true;
+                }
+            }
+            if (!moved) {
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) {
+                    g_st(p.abort_word, 1u);
+                    break;
+                }
+                if (!spin_ok(spins, limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
+            } else {
+                spins = 0;
+            }
+        }
+        return;
+    }
+    if (w >= nlive) return;
+
+    // ---------------- compute wave w: stripe s, columns j0+1 .. j0+64*TD ----------------
+    __builtin_amdgcn_s_setprio(2);
+    const int s = g * NWC + w;
+    const int j0 = s * 64 * TD;
+    const int jl = j0 + lane * TD;  // this lane: columns jl+1 .. jl+TD
+    const bool partial = j0 + 64 * TD > p.n;
+    const int cn = p.n - 1 - j0;    // column n's offset in a partial stripe
+    const int tm = partial ? m - 1 + cn / TD : -1;  // the step at which its lane reaches row m
+    const int ck = cn % TD;
+    int Hm = 0;
+    int H[TD], Y[TD];
+    unsigned qb[TD];  // dword index of each column's code row in the profile table
+#pragma unroll
+    for (int k = 0; k < TD; k++) {
+        const int jc = jl + k + 1;
+        const bool ok = jc <= p.n;
+        const int2 t = p.top[ok ? jc : p.n];
+        H[k] = t.x;  // H'(0, j) until the lane reaches row 1
+        Y[k] = t.y;  // h2'(0, j)
+        qb[k] = (unsigned)((ok ? p.b[jc - 1] : 0) * QS);
+    }
+    int HLp = p.top[min(jl, p.n)].x;  // lane 0: H'(0, j0), the diagonal of row 1
+    int Hl = H[TD - 1], Xl = 0, RH = 0, RX = 0;
+    const int2* rin = ring + w * RING;
+    int2* rout = ring + (w + 1) * RING;
+    unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
+    unsigned* cons_out = &cnt[2 * w + 2];
+    const unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
+    const unsigned rout_lds = lds_addr(rout);
+    unsigned avail = 0, outfree = 0, qavail = 0;
+    bool aborted = false;
+    unsigned long long wcyc[3] = {0, 0, 0}, t_start = 0, c_start = 0;
+    if (DBG) {
+        t_start = __builtin_amdgcn_s_memrealtime();
+        c_start = __builtin_amdgcn_s_memtime();
+    }
+    auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target, int kind) {
+        unsigned spins = 0;
+        cached = sgpr_u(cached);
+        unsigned long long t0 = 0;
+        if (DBG && (int)cached < target) t0 = __builtin_amdgcn_s_memtime();
+        while ((int)cached < target && !aborted) {
+            cached = lds_ldu(ctr) + add;
+            if ((int)cached >= target) break;
+            if (!spin_ok_lds(spins, p.spin_limit, abort_sh)) aborted = true;
+        }
+        if (DBG && t0) wcyc[kind] += __builtin_amdgcn_s_memtime() - t0;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    };
+    // sub-chunk 0: lane 0's rows 1..8 (slots 0..7), the lanes' profile windows
+    int4 A[4], B[4];
+    uint32_t qA[TD][2], qB[TD][2];
+    wait_ge(prod_in, 0, avail, LK_SUB, 0);
+#pragma unroll
+    for (int k = 0; k < 4; k++) A[k] = reinterpret_cast<const int4*>(rin)[k];
+    wait_ge(&cnt[LK_PRODQ], 0, qavail, LK_SUB, 1);
+    {
+        const unsigned idx = (unsigned)(-lane) & qmask;
+#pragma unroll
+        for (int k = 0; k < TD; k++) {
+            qA[k][0] = pq[qb[k] + idx];
+            qA[k][1] = pq[qb[k] + idx + 4];
+        }
+    }
+    unsigned pnext = *prod_in;  // the producer's counter, read a sub-chunk before it is needed
+    const unsigned long long out_mask = 0xff00000000000000ull;  // lanes 56..63: the shift registers' rows
+
+    // one 8-step sub-chunk: steps r0 .. r0+7 from C / qc; after its first step the next sub-chunk's
+    // edges, profile windows and the producer's counter are read into Nx / qx / pnext (they land while
+    // steps 1..7 run); then lanes 56..63 store lane 63's eight rows and lane 0 publishes
+    // {cons(w) = r0 + 16, prod(w + 1)} in one 8-byte store
+    auto sub_chunk = [&](int r0, int4 (&C)[4], int4 (&Nx)[4], uint32_t (&qc)[TD][2], uint32_t (&qx)[TD][2]) {
+        avail = sgpr_u(max(avail, pnext));
+        if ((int)avail < r0 + 2 * LK_SUB) wait_ge(prod_in, 0, avail, r0 + 2 * LK_SUB, 0);
+        if ((int)qavail < r0 + 2 * LK_SUB) wait_ge(&cnt[LK_PRODQ], 0, qavail, r0 + 2 * LK_SUB, 1);
+        const int eh[8] = {C[0].x, C[0].z, C[1].x, C[1].z, C[2].x, C[2].z, C[3].x, C[3].z};
+        const int ex[8] = {C[0].y, C[0].w, C[1].y, C[1].w, C[2].y, C[2].w, C[3].y, C[3].w};
+        uint32_t qa[TD], qd[TD];  // rows r0-l+1 .. +4 and r0-l+5 .. +8 of each column
+#pragma unroll
+        for (int k = 0; k < TD; k++) { qa[k] = qc[k][0]; qd[k] = qc[k][1]; }
+        auto loads = [&]() {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 4; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + LK_SUB) & RMASK))[k];
+            const unsigned idx = (unsigned)(r0 + LK_SUB - lane) & qmask;
+#pragma unroll
+            for (int k = 0; k < TD; k++) {
+                qx[k][0] = pq[qb[k] + idx];
+                qx[k][1] = pq[qb[k] + idx + 4];
+            }
+            pnext = __hip_atomic_load(prod_in, RLX, WGS);
+            asm volatile("" ::: "memory");
+        };
+        if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)LK_SUB) {
+            const int row0 = r0 - lane + 1;
+            const bool capl = lane == cn / TD;
+#define LK_MSTEP(U, QQ, UU) \
+    lane_step_masked<TD, U>(H, Y, Xl, Hl, HLp, RH, RX, eh[UU], ex[UU], QQ, o, row0 + UU, capl && r0 + UU == tm, ck, Hm)
+            LK_MSTEP(0, qa, 0);
+            loads();
+            LK_MSTEP(1, qa, 1); LK_MSTEP(2, qa, 2); LK_MSTEP(3, qa, 3);
+            LK_MSTEP(0, qd, 4); LK_MSTEP(1, qd, 5); LK_MSTEP(2, qd, 6); LK_MSTEP(3, qd, 7);
+#undef LK_MSTEP
+        } else {
+            lane_step<TD, 0>(H, Y, Xl, Hl, HLp, RH, RX, eh[0], ex[0], qa, o);
+            loads();
+            lane_step<TD, 1>(H, Y, Xl, Hl, HLp, RH, RX, eh[1], ex[1], qa, o);
+            lane_step<TD, 2>(H, Y, Xl, Hl, HLp, RH, RX, eh[2], ex[2], qa, o);
+            lane_step<TD, 3>(H, Y, Xl, Hl, HLp, RH, RX, eh[3], ex[3], qa, o);
+            lane_step<TD, 0>(H, Y, Xl, Hl, HLp, RH, RX, eh[4], ex[4], qd, o);
+            lane_step<TD, 1>(H, Y, Xl, Hl, HLp, RH, RX, eh[5], ex[5], qd, o);
+            lane_step<TD, 2>(H, Y, Xl, Hl, HLp, RH, RX, eh[6], ex[6], qd, o);
+            lane_step<TD, 3>(H, Y, Xl, Hl, HLp, RH, RX, eh[7], ex[7], qd, o);
+        }
+        // lane 63 computed rows r0-62 .. r0-55; lanes 56..63 of the shift registers hold them
+        const int rlo = r0 - 62;
+        if ((int)outfree < rlo + LK_SUB - 1) wait_ge(cons_out, RING, outfree, rlo + LK_SUB - 1, 2);
+        const unsigned oaddr = rout_lds + (unsigned)((rlo - 57 + lane) & RMASK) * 8u;
+        typedef int v2i_t __attribute__((ext_vector_type(2)));
+        const v2i_t hx = {RH, RX};
+        const lk_v2u cp = {(unsigned)(r0 + 2 * LK_SUB), (unsigned)max(rlo + LK_SUB - 1, 0)};
+        unsigned long long saved;
+        asm volatile(
+            "s_mov_b64 %0, exec\n\t"
+            "s_mov_b64 exec, %4\n\t"
+            "ds_write_b64 %1, %2\n\t"
+            "s_mov_b64 exec, 1\n\t"
+            "ds_write_b64 %3, %5\n\t"
+            "s_mov_b64 exec, %0\n\t"
+            "s_nop 4"
+            : "=&s"(saved)
+            : "v"(oaddr), "v"(hx), "v"(pc_lds), "s"(out_mask), "v"(cp)
+            : "memory");
+    };
+    const int nsub2 = (nsub + 1) & ~1;  // whole pairs (the extra steps run past row m: garbage nobody reads)
+    for (int sc = 0; sc < nsub2; sc += 2) {
+        const int r0 = __builtin_amdgcn_readfirstlane(sc * LK_SUB);
+        sub_chunk(r0, A, B, qA, qB);
+        sub_chunk(r0 + LK_SUB, B, A, qB, qA);
+    }
+    unsigned* prod_out = &cnt[2 * w + 1];
+    if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
+    if (partial && lane == cn / TD) p.out_last[0] = Hm;
+    if (DBG && lane == 0) {
+        unsigned long long* d = p.dbg + 8 * s;
+        d[0] = t_start;
+        d[1] = __builtin_amdgcn_s_memrealtime();
+        d[2] = wcyc[0];
+        d[3] = wcyc[1];
+        d[4] = wcyc[2];
+        d[5] = __builtin_amdgcn_s_memtime() - c_start;
+        d[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID: wave, SIMD, CU, SE
+        d[7] = 0;
+    }
+}
+
+template <int NWC, int TD, bool DBG = false>
+static void launch_lane_one(hipStream_t s, const FillArgs& p) {
+    if (!DBG && p.dbg != nullptr) return launch_lane_one<NWC, TD, true>(s, p);
+    const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), (size_t)FILL_LDS_MIN);
+    auto* fn = fill_lane_kernel<NWC, TD, DBG>;
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+}
+
+template <int TD>
+static void launch_lane_td(hipStream_t s, const FillArgs& p) {
+    if (p.nwc == 4) launch_lane_one<4, TD>(s, p);
+    else launch_lane_one<8, TD>(s, p);
+}
+
+void launch_fill_lane(hipStream_t s, const FillArgs& p) {
+    switch (p.cols_per_lane) {
+        case 1: launch_lane_td<1>(s, p); break;
+        case 2: launch_lane_td<2>(s, p); break;
+        case 4: launch_lane_td<4>(s, p); break;
+        default: launch_lane_td<8>(s, p); break;
+    }
+}
+
+}  // namespace ga

@@ -34,8 +34,9 @@ import time
 import numpy as np
 
 
-def slab_bounds(n, world, align=256):
-    """Contiguous column slabs [c_k, c_{k+1}); inner edges on multiples of `align` when n allows."""
+def slab_bounds(n, world, align=512):
+    """Contiguous column slabs [c_k, c_{k+1}); inner edges on multiples of `align` when n allows (512: an
+    inner slab ends on a whole stripe of either fill kernel at any stripe width)."""
     if world < 1 or n < world:
         raise ValueError(f"cannot split {n} columns over {world} ranks")
     edges = [0]

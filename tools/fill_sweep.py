@@ -3,7 +3,8 @@
     python tools/fill_sweep.py m n K tb(0|1)
 
 Prints one JSON line: cost, per-launch fill ms (HIP events), cells/s.  Used to sweep launch
-settings given through the environment (GA_FILL_LDS_FLOOR)."""
+settings given through the environment (GA_FILL_MODE, GA_LANE_COLS_PER_LANE, GA_FILL_NWC,
+GA_FILL_LDS_FLOOR)."""
 import json
 import os
 import sys
@@ -23,5 +24,6 @@ for _ in range(K):
     cost, _ = eng.fill(traceback=bool(tb))
     ms.append(eng.kernel_ms()[0])
 best = min(ms[1:] if K > 1 else ms)
-print(json.dumps({"m": m, "n": n, "tb": tb, "floor": os.environ.get("GA_FILL_LDS_FLOOR"), "cost": int(cost),
+print(json.dumps({"m": m, "n": n, "tb": tb, "kind": eng.fill_kind(), "mode": os.environ.get("GA_FILL_MODE"),
+                  "floor": os.environ.get("GA_FILL_LDS_FLOOR"), "cost": int(cost),
                   "fill_ms": ms, "best_cells_per_s": m * n / (best * 1e-3)}), flush=True)

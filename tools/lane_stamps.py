@@ -1,0 +1,68 @@
+"""Diagnostic: per-stripe timestamps of one lane-skewed fill (fill_lane_kernel DBG variant).
+
+    GA_FILL_MODE=lane python tools/lane_stamps.py [m] [n]
+
+Prints one JSON line: the fill time, the chain's start lags (intra- and cross-workgroup), stripe
+durations, and the cycles each stripe waited for its left edge / the profile / ring space, grouped by
+the SIMD the wave ran on (HW_ID bits 5:4) -- a chain runs at its slowest stripe's pace, and that
+stripe is the one that never waits for its left neighbour."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from globalign_amd import _native  # noqa: E402
+
+m = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 125_000
+s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
+tables, _ = bench.problem_tables(s1, s2)
+eng = _native.Engine(0)
+eng.load(tables.codes(s1), tables.codes(s2), tables)
+L = _native.load_library()
+L.ga_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64]
+eng.fill(traceback=False)
+plain_ms = eng.kernel_ms()[0]
+L.ga_debug_stamps(eng._h, 1, None, 0)
+cost, _ = eng.fill(traceback=False)
+kind, T, ns, nwc, nslabs = eng.fill_kind()
+buf = np.zeros(8 * ns, dtype=np.uint64)
+L.ga_debug_stamps(eng._h, 0, buf.ctypes.data, buf.size)
+L.ga_debug_stamps(eng._h, 0, None, 0)
+st = buf.reshape(ns, 8).astype(np.int64)
+t0 = st[:, 0].min()
+start, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0  # microseconds (100 MHz)
+dur = end - start
+tot = np.maximum(st[:, 5], 1)
+simd = (st[:, 6] >> 4) & 3
+wave_in_wg = np.arange(ns) % nwc
+lag = np.diff(start)
+cross = np.array([(k + 1) % nwc == 0 for k in range(ns - 1)], dtype=bool)
+by_simd = {}
+for sd in range(4):
+    sel = simd == sd
+    if sel.any():
+        by_simd[int(sd)] = {"stripes": int(sel.sum()), "dur_us_median": float(np.median(dur[sel])),
+                            "wait_edge_frac": float(np.median(st[sel, 2] / tot[sel])),
+                            "wait_prof_frac": float(np.median(st[sel, 3] / tot[sel])),
+                            "wait_space_frac": float(np.median(st[sel, 4] / tot[sel])),
+                            "cyc_per_step_busy": float(np.median((tot[sel] - st[sel, 2] - st[sel, 3] - st[sel, 4]) /
+                                                                 (m + 63)))}
+by_wave = {int(w): {"wait_edge_frac": float(np.median(st[wave_in_wg == w, 2] / tot[wave_in_wg == w])),
+                    "simd_mode": int(np.bincount(simd[wave_in_wg == w]).argmax())} for w in range(min(nwc, ns))}
+print(json.dumps({
+    "m": m, "n": n, "cost": int(cost), "kind": kind, "TD": T, "nstripes": ns, "nwc": nwc, "nslabs": nslabs,
+    "fill_ms_plain": plain_ms, "fill_ms_dbg": eng.kernel_ms()[0],
+    "last_end_us": float(end.max()), "last_start_us": float(start.max()),
+    "lag_intra_wg_us": float(np.mean(lag[~cross])) if (~cross).any() else None,
+    "lag_cross_wg_us": float(np.mean(lag[cross])) if cross.any() else None,
+    "stripe_dur_us_median": float(np.median(dur)), "stripe_dur_us_max": float(dur.max()),
+    "ns_per_step_median": float(np.median(dur) * 1e3 / (m + 63)),
+    "cycles_per_step_median": float(np.median(tot / (m + 63))),
+    "by_simd": by_simd, "by_wave": by_wave,
+}), flush=True)
