@@ -79,9 +79,9 @@ void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, 
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)
 void launch_fill_diag(hipStream_t s, const FillArgs& p, int qbytes, bool full);
 size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows);
-// score-only lane-skewed anti-diagonal fill (ga_lane.hip; FillArgs.cols_per_lane = TD in {1, 2, 4, 8},
-// int8 profile, K <= 32, qrows = profile table rows, a power of two)
-void launch_fill_lane(hipStream_t s, const FillArgs& p);
+// lane-skewed anti-diagonal fill (ga_lane.hip; FillArgs.cols_per_lane = TD in {1, 2, 4, 8}, <= 4 with
+// traceback words (p.tb != nullptr, CB bytes per cell), int8 profile, K <= 32, qrows = profile rows, a power of two)
+void launch_fill_lane(hipStream_t s, const FillArgs& p, int CB);
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows);
 
 }  // namespace ga

@@ -403,8 +403,8 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full, int64_t ncols = -1) {
 // step per wave at one / two waves per SIMD, with the kernel's per-step LDS traffic and the DPP
 // shift-register output) times the chain's length, m steps plus ~74 steps of skew per stripe.
 // Returns false (row scan) when the profile table does not fit beside the rings.
-bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out) {
-    if (c->qbytes != 1 || c->K > 32 || c->CB < 1) return false;
+bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
+    if (c->qbytes != 1 || c->K > 32) return false;
     static const double cyc[4][2] = {{61, 105}, {89, 160}, {131, 245}, {226, 423}};  // TD = 1, 2, 4, 8
     const int64_t cus = c->num_cu;
     int bestT = 0, bestN = 0;
@@ -412,10 +412,14 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out) {
     for (int ti = 0; ti < 4; ti++) {
         const int T = 1 << ti;
         if (c->lane_T_req && c->lane_T_req != T) continue;
+        // traceback windows (register budget, ga_lane.hip lane_variant_ok): TD <= 4 with one-byte
+        // words, <= 2 with two- and four-byte words (four-byte: 4 waves per workgroup)
+        if (tb && T > (c->CB == 1 ? 4 : 2)) continue;
         // a slab with a right neighbour hands column n on: its last stripe must be whole
         if (c->col0 + c->n < c->n_global && ncol % (64 * T) != 0) continue;
         const int64_t ns = (ncol + 64 * T - 1) / (64 * T);
         const int nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : ns <= 4 * cus ? 4 : 8;
+        if (tb && c->CB == 4 && nwc == 8) continue;
         if (ns > nwc * cus) continue;  // not every stripe resident
         const int wps = (ns + 4 * cus - 1) / (4 * cus) > 1 ? 1 : 0;
         const double t = ((double)c->m + 74.0 * (double)ns) * cyc[ti][wps];
@@ -426,8 +430,13 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out) {
         }
     }
     if (!bestT) return false;
+    // GA_LANE_QROWS caps the profile table (tuning: a smaller table lets two workgroups share a CU)
+    static const int qcap = [] {
+        const char* e = getenv("GA_LANE_QROWS");
+        return e ? atoi(e) : 4096;
+    }();
     const size_t budget = 150 * 1024;
-    int qr = 4096;
+    int qr = std::max(256, std::min(4096, qcap));
     while (qr > 256 && ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget) qr >>= 1;
     if (ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget || qr < bestN * 64 + 192) return false;
     c->T = bestT;
@@ -573,8 +582,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // score only: the lane-skewed kernel when its chain's skew (~74 steps per stripe)
     // is short against the m rows every stripe walks (measured: 1M x 125k 60 ms against 107 for the row
     // scan, C4 244 against 312; 100k x 100k, whose 782 stripes add 58k steps of skew, 13.5 against 12.6)
-    if (!tb && !bd.band && bd.ckpt == nullptr && (c->diag_req == 3 || c->diag_req == 0) && lane_geometry(c, n, &qrows) &&
-        (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
+    if (!full && bd.ckpt == nullptr && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
+        lane_geometry(c, n, &qrows, tb) && (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
         c->lane = true;
     // automatic: score-only fills of tall problems on one GPU (m >= 4 n, <= 8 stripes per CU).
     // Measured (profiles/r01/diag_sweep.txt): 1M x 125k 80 ms (TD = 1) against 107 ms for the row
@@ -665,7 +674,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
-    if (c->lane) ga::launch_fill_lane(st, p);
+    if (c->lane) ga::launch_fill_lane(st, p, c->CB);
     else if (c->diag) ga::launch_fill_diag(st, p, c->qbytes, full);
     else ga::launch_fill(st, p, c->CB, c->qbytes, tb, full);
     HIPCHK(hipGetLastError());

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ga_device.h"
 #include "ga_sync.h"
@@ -46,22 +47,45 @@ size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
            (size_t)K * 32;  // + the K x K int8 sub' table (K <= 32)
 }
 
-// one step of the fast path; U: the step's byte in the profile dwords
-template <int TD, int U>
+// traceback code of a cell (CB bytes, W = (8*CB-1)/2 bits per field; fill_kernel's TbFmt): the
+// saturated X'-H', Y'-H' and M' != H', all dp_array_backward's rank test needs
+template <int CB>
+__device__ __forceinline__ unsigned lk_code(int M, int X, int Y, int H, unsigned op1) {
+    constexpr int W = (8 * CB - 1) / 2;
+    return min((unsigned)(X - H), op1) | (min((unsigned)(Y - H), op1) << W) | (min((unsigned)(M - H), 1u) << (2 * W));
+}
+// a cell's code into byte UU*CB of its column's 16-step window
+template <int CB, int UU>
+__device__ __forceinline__ void lk_put(uint32_t (&acc)[4 * (CB > 0 ? CB : 1)], unsigned code) {
+    if constexpr (CB > 0) {
+        constexpr int bo = UU * CB, dw = bo >> 2, sh = (bo & 3) * 8;
+        if constexpr (sh == 0) acc[dw] = code;
+        else acc[dw] |= code << sh;
+    }
+}
+
+// one step; U: the step's byte in the profile dwords; CB > 0: traceback codes into window byte UU*CB;
+// MASKED: lanes above row 1 keep their row-0 state, and a partial stripe captures H'(m, n) into Hm
+template <int TD, int U, int CB, int UU, bool MASKED>
 __device__ __forceinline__ void lane_step(int (&H)[TD], int (&Y)[TD], int& Xl, int& Hl, int& HLp, int& RH, int& RX,
-                                          int eh, int ex, const uint32_t (&q)[TD], int o) {
+                                          int eh, int ex, const uint32_t (&q)[TD], int o,
+                                          uint32_t (&acc)[TD][4 * (CB > 0 ? CB : 1)], unsigned op1, int row, bool cap,
+                                          int ck, int& Hm) {
     int X = __builtin_amdgcn_update_dpp(ex, Xl, 0x138, 0xf, 0xf, false);          // h1'(i, left): lane 0 the edge
     const int HLn = __builtin_amdgcn_update_dpp(eh, Hl, 0x138, 0xf, 0xf, false);  // H'(i, left), the next diagonal
+    const bool act = !MASKED || row >= 1;
     int Hd = HLp;
 #pragma unroll
     for (int k = 0; k < TD; k++) {
         const int M = Hd + (int)(int8_t)(q[k] >> (8 * U));
         const int Hn = min(min(M, X), Y[k]);
         const int Ho = Hn + o;
+        if constexpr (CB > 0) lk_put<CB, UU>(acc[k], lk_code<CB>(M, X, Y[k], Hn, op1));
         X = min(X, Ho);
-        Y[k] = min(Y[k], Ho);
+        if (MASKED && cap && k == ck) Hm = Hn;
+        Y[k] = act ? min(Y[k], Ho) : Y[k];
         Hd = H[k];
-        H[k] = Hn;
+        H[k] = act ? Hn : H[k];
     }
     Xl = X;
     Hl = H[TD - 1];
@@ -70,37 +94,53 @@ __device__ __forceinline__ void lane_step(int (&H)[TD], int (&Y)[TD], int& Xl, i
     RX = __builtin_amdgcn_update_dpp(Xl, RX, 0x130, 0xf, 0xf, false);
 }
 
-// the masked step of the first sub-chunks (lanes above row 1 keep their row-0 state) and of the
-// sub-chunk in which a partial stripe's column n reaches row m (captured into Hm)
-template <int TD, int U>
-__device__ __forceinline__ void lane_step_masked(int (&H)[TD], int (&Y)[TD], int& Xl, int& Hl, int& HLp, int& RH,
-                                                 int& RX, int eh, int ex, const uint32_t (&q)[TD], int o, int row,
-                                                 bool cap, int ck, int& Hm) {
-    int X = __builtin_amdgcn_update_dpp(ex, Xl, 0x138, 0xf, 0xf, false);
-    const int HLn = __builtin_amdgcn_update_dpp(eh, Hl, 0x138, 0xf, 0xf, false);
-    const bool act = row >= 1;
-    int Hd = HLp;
+// End of a 16-step window c of traceback codes.  Byte u*CB of lane l's window holds row 16c+u-l+1
+// (the lane skew), so with phi = l mod 16 the window rotated by phi cells, R_c, holds at cell
+// position p < 16-phi row 16(c-l/16)+p+1 and at p >= 16-phi the row 16 earlier: the aligned word
+// a = c-1-l/16 (rows 16a+1 .. 16a+16, the layout fill_kernel writes and the walk reads) is R_(c-1)
+// below 16-phi and R_c above.  Per column: log2(4CB) dword-rotation stages (per-lane v_cndmask),
+// 4CB v_alignbyte for the byte remainder, 4CB v_bfi for the merge, CB 16-byte stores.
+template <int TD, int CB>
+struct LkRot {
+    static constexpr int N = 4 * CB;  // dwords per window
+    bool qbit[4];                     // dword rotation (phi*CB / 4) bits
+    unsigned rb;                      // byte remainder (phi*CB & 3)
+    uint32_t mask[N];                 // bytes below CB*(16-phi): from R_(c-1)
+    __device__ __forceinline__ void init(int phi) {
+        const int q = (phi * CB) >> 2;
 #pragma unroll
-    for (int k = 0; k < TD; k++) {
-        const int M = Hd + (int)(int8_t)(q[k] >> (8 * U));
-        const int Hn = min(min(M, X), Y[k]);
-        const int Ho = Hn + o;
-        X = min(X, Ho);
-        if (cap && k == ck) Hm = Hn;
-        Y[k] = act ? min(Y[k], Ho) : Y[k];
-        Hd = H[k];
-        H[k] = act ? Hn : H[k];
+        for (int b = 0; b < 4; b++) qbit[b] = ((q >> b) & 1) != 0;
+        rb = (unsigned)((phi * CB) & 3);
+        const int lowb = CB * (16 - phi);
+#pragma unroll
+        for (int d = 0; d < N; d++) {
+            uint32_t mk = 0;
+#pragma unroll
+            for (int y = 0; y < 4; y++) mk |= (4 * d + y < lowb) ? (0xffu << (8 * y)) : 0u;
+            mask[d] = mk;
+        }
     }
-    Xl = X;
-    Hl = H[TD - 1];
-    HLp = HLn;
-    RH = __builtin_amdgcn_update_dpp(Hl, RH, 0x130, 0xf, 0xf, false);
-    RX = __builtin_amdgcn_update_dpp(Xl, RX, 0x130, 0xf, 0xf, false);
-}
+    __device__ __forceinline__ void rotate(const uint32_t (&w)[N], uint32_t (&r)[N]) const {
+        uint32_t v[N];
+#pragma unroll
+        for (int d = 0; d < N; d++) v[d] = w[d];
+#pragma unroll
+        for (int b = 0; (1 << b) < N; b++) {
+            uint32_t t[N];
+#pragma unroll
+            for (int d = 0; d < N; d++) t[d] = qbit[b] ? v[(d + (1 << b)) % N] : v[d];
+#pragma unroll
+            for (int d = 0; d < N; d++) v[d] = t[d];
+        }
+#pragma unroll
+        for (int d = 0; d < N; d++) r[d] = __builtin_amdgcn_alignbyte(v[(d + 1) % N], v[d], rb);
+    }
+};
 
 // DBG: per stripe {start, end (s_memrealtime), cycles waiting for edges / profile / ring space,
 // total cycles, HW_ID} into p.dbg (tools/lane_stamps.py)
-template <int NWC, int TD, bool DBG>
+// CB > 0: traceback words (CB bytes per cell) into p.tb in fill_kernel's aligned layout
+template <int NWC, int TD, int CB, bool DBG>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -122,7 +162,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     const int g = __builtin_amdgcn_readfirstlane((int)cnt[LK_SLAB]);
     const int m = p.m, o = p.o;
     const int nsteps = m + 63;  // lane 63 reaches row m at step m + 62
-    const int nsub = (nsteps + LK_SUB - 1) / LK_SUB;
+    // 16-step windows (pairs of sub-chunks); with traceback words the last aligned word
+    // (ceil(m/16) - 1) leaves lanes 48..63 at window ceil(m/16) + 3 (LkRot)
+    const int tca = (m + 15) / 16;
+    const int npairs = CB > 0 ? tca + 4 : (nsteps + 2 * LK_SUB - 1) / (2 * LK_SUB);
     const int nlive = min(NWC, p.nstripes - g * NWC);
 
     if (w == NWC) {
@@ -261,13 +304,30 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         Y[k] = t.y;  // h2'(0, j)
         qb[k] = (unsigned)((ok ? p.b[jc - 1] : 0) * QS);
     }
+    // traceback words: column (lane, k) is lane p = (lane*TD + k) mod 64 of 64-column stripe
+    // TD*s + (lane*TD + k) / 64 (as for fill_kernel's blocked stripes)
+    constexpr int CBX = CB > 0 ? CB : 1;
+    uint32_t acc[TD][4 * CBX], prevw[TD][4 * CBX];
+    uint4* colw[TD];
+    LkRot<TD, CBX> rot;
+    const unsigned op1 = (unsigned)o + 1u;
+    if constexpr (CB > 0) {
+        rot.init(lane & 15);
+#pragma unroll
+        for (int k = 0; k < TD; k++) {
+            const int c = lane * TD + k;
+            colw[k] = reinterpret_cast<uint4*>(p.tb) + ((long long)(TD * s + c / 64) * p.TC) * 64 + (c & 63);
+#pragma unroll
+            for (int d = 0; d < 4 * CBX; d++) prevw[k][d] = 0;
+        }
+    }
     int HLp = p.top[min(jl, p.n)].x;  // lane 0: H'(0, j0), the diagonal of row 1
     int Hl = H[TD - 1], Xl = 0, RH = 0, RX = 0;
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
     unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
     unsigned* cons_out = &cnt[2 * w + 2];
-    const unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
+    unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
     unsigned avail = 0, outfree = 0, qavail = 0;
     bool aborted = false;
@@ -305,13 +365,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         }
     }
     unsigned pnext = *prod_in;  // the producer's counter, read a sub-chunk before it is needed
-    const unsigned long long out_mask = 0xff00000000000000ull;  // lanes 56..63: the shift registers' rows
+    unsigned long long out_mask = 0xff00000000000000ull;  // lanes 56..63: the shift registers' rows
 
     // one 8-step sub-chunk: steps r0 .. r0+7 from C / qc; after its first step the next sub-chunk's
     // edges, profile windows and the producer's counter are read into Nx / qx / pnext (they land while
     // steps 1..7 run); then lanes 56..63 store lane 63's eight rows and lane 0 publishes
     // {cons(w) = r0 + 16, prod(w + 1)} in one 8-byte store
-    auto sub_chunk = [&](int r0, int4 (&C)[4], int4 (&Nx)[4], uint32_t (&qc)[TD][2], uint32_t (&qx)[TD][2]) {
+    auto sub_chunk = [&](int r0, int4 (&C)[4], int4 (&Nx)[4], uint32_t (&qc)[TD][2], uint32_t (&qx)[TD][2], auto HALF) {
+        constexpr int HB = decltype(HALF)::value * LK_SUB;  // the sub-chunk's first step in its 16-step window
         avail = sgpr_u(max(avail, pnext));
         if ((int)avail < r0 + 2 * LK_SUB) wait_ge(prod_in, 0, avail, r0 + 2 * LK_SUB, 0);
         if ((int)qavail < r0 + 2 * LK_SUB) wait_ge(&cnt[LK_PRODQ], 0, qavail, r0 + 2 * LK_SUB, 1);
@@ -333,27 +394,23 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             pnext = __hip_atomic_load(prod_in, RLX, WGS);
             asm volatile("" ::: "memory");
         };
+        const int row0 = r0 - lane + 1;
+        const bool capl = lane == cn / TD;
+#define LK_STEP(MK, U, QQ, UU)                                                                               \
+    lane_step<TD, U, CB, HB + UU, MK>(H, Y, Xl, Hl, HLp, RH, RX, eh[UU], ex[UU], QQ, o, acc, op1, row0 + UU, \
+                                       capl && r0 + UU == tm, ck, Hm)
         if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)LK_SUB) {
-            const int row0 = r0 - lane + 1;
-            const bool capl = lane == cn / TD;
-#define LK_MSTEP(U, QQ, UU) \
-    lane_step_masked<TD, U>(H, Y, Xl, Hl, HLp, RH, RX, eh[UU], ex[UU], QQ, o, row0 + UU, capl && r0 + UU == tm, ck, Hm)
-            LK_MSTEP(0, qa, 0);
+            LK_STEP(true, 0, qa, 0);
             loads();
-            LK_MSTEP(1, qa, 1); LK_MSTEP(2, qa, 2); LK_MSTEP(3, qa, 3);
-            LK_MSTEP(0, qd, 4); LK_MSTEP(1, qd, 5); LK_MSTEP(2, qd, 6); LK_MSTEP(3, qd, 7);
-#undef LK_MSTEP
+            LK_STEP(true, 1, qa, 1); LK_STEP(true, 2, qa, 2); LK_STEP(true, 3, qa, 3);
+            LK_STEP(true, 0, qd, 4); LK_STEP(true, 1, qd, 5); LK_STEP(true, 2, qd, 6); LK_STEP(true, 3, qd, 7);
         } else {
-            lane_step<TD, 0>(H, Y, Xl, Hl, HLp, RH, RX, eh[0], ex[0], qa, o);
+            LK_STEP(false, 0, qa, 0);
             loads();
-            lane_step<TD, 1>(H, Y, Xl, Hl, HLp, RH, RX, eh[1], ex[1], qa, o);
-            lane_step<TD, 2>(H, Y, Xl, Hl, HLp, RH, RX, eh[2], ex[2], qa, o);
-            lane_step<TD, 3>(H, Y, Xl, Hl, HLp, RH, RX, eh[3], ex[3], qa, o);
-            lane_step<TD, 0>(H, Y, Xl, Hl, HLp, RH, RX, eh[4], ex[4], qd, o);
-            lane_step<TD, 1>(H, Y, Xl, Hl, HLp, RH, RX, eh[5], ex[5], qd, o);
-            lane_step<TD, 2>(H, Y, Xl, Hl, HLp, RH, RX, eh[6], ex[6], qd, o);
-            lane_step<TD, 3>(H, Y, Xl, Hl, HLp, RH, RX, eh[7], ex[7], qd, o);
+            LK_STEP(false, 1, qa, 1); LK_STEP(false, 2, qa, 2); LK_STEP(false, 3, qa, 3);
+            LK_STEP(false, 0, qd, 4); LK_STEP(false, 1, qd, 5); LK_STEP(false, 2, qd, 6); LK_STEP(false, 3, qd, 7);
         }
+#undef LK_STEP
         // lane 63 computed rows r0-62 .. r0-55; lanes 56..63 of the shift registers hold them
         const int rlo = r0 - 62;
         if ((int)outfree < rlo + LK_SUB - 1) wait_ge(cons_out, RING, outfree, rlo + LK_SUB - 1, 2);
@@ -362,6 +419,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         const v2i_t hx = {RH, RX};
         const lk_v2u cp = {(unsigned)(r0 + 2 * LK_SUB), (unsigned)max(rlo + LK_SUB - 1, 0)};
         unsigned long long saved;
+        const unsigned pcl = pc_lds;            // (a generic lambda's asm operands must be its own locals)
+        const unsigned long long om = out_mask;
         asm volatile(
             "s_mov_b64 %0, exec\n\t"
             "s_mov_b64 exec, %4\n\t"
@@ -371,14 +430,36 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             "s_mov_b64 exec, %0\n\t"
             "s_nop 4"
             : "=&s"(saved)
-            : "v"(oaddr), "v"(hx), "v"(pc_lds), "s"(out_mask), "v"(cp)
+            : "v"(oaddr), "v"(hx), "v"(pcl), "s"(om), "v"(cp)
             : "memory");
     };
-    const int nsub2 = (nsub + 1) & ~1;  // whole pairs (the extra steps run past row m: garbage nobody reads)
-    for (int sc = 0; sc < nsub2; sc += 2) {
-        const int r0 = __builtin_amdgcn_readfirstlane(sc * LK_SUB);
-        sub_chunk(r0, A, B, qA, qB);
-        sub_chunk(r0 + LK_SUB, B, A, qB, qA);
+    // whole 16-step windows (steps past row m compute garbage nobody reads)
+    for (int pr = 0; pr < npairs; pr++) {
+        const int r0 = __builtin_amdgcn_readfirstlane(pr * 2 * LK_SUB);
+        sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
+        sub_chunk(r0 + LK_SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
+        if constexpr (CB > 0) {
+            // window pr done: aligned word pr - 1 - lane/16 of every column (LkRot)
+            const int a = pr - 1 - (lane >> 4);
+            const bool st = a >= 0 && a < tca;
+#pragma unroll
+            for (int k = 0; k < TD; k++) {
+                uint32_t r[4 * CBX];
+                rot.rotate(acc[k], r);
+                uint32_t wd[4 * CBX];
+#pragma unroll
+                for (int d = 0; d < 4 * CBX; d++) {
+                    wd[d] = (prevw[k][d] & rot.mask[d]) | (r[d] & ~rot.mask[d]);
+                    prevw[k][d] = r[d];
+                }
+                if (st) {
+#pragma unroll
+                    for (int d = 0; d < CBX; d++)
+                        colw[k][(long long)(a * CBX + d) * 64] =
+                            make_uint4(wd[4 * d], wd[4 * d + 1], wd[4 * d + 2], wd[4 * d + 3]);
+                }
+            }
+        }
     }
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
@@ -396,28 +477,53 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     }
 }
 
-template <int NWC, int TD, bool DBG = false>
+template <int NWC, int TD, int CB, bool DBG = false>
 static void launch_lane_one(hipStream_t s, const FillArgs& p) {
-    if (!DBG && p.dbg != nullptr) return launch_lane_one<NWC, TD, true>(s, p);
-    const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), (size_t)FILL_LDS_MIN);
-    auto* fn = fill_lane_kernel<NWC, TD, DBG>;
+    if constexpr (!DBG && CB == 0)
+        if (p.dbg != nullptr) return launch_lane_one<NWC, TD, CB, true>(s, p);
+    // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
+    static const long floor_env = [] {
+        const char* e = getenv("GA_FILL_LDS_FLOOR");
+        return e ? atol(e) : -1L;
+    }();
+    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
+    auto* fn = fill_lane_kernel<NWC, TD, CB, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
 
-template <int TD>
-static void launch_lane_td(hipStream_t s, const FillArgs& p) {
-    if (p.nwc == 4) launch_lane_one<4, TD>(s, p);
-    else launch_lane_one<8, TD>(s, p);
+// variants without spills (vgpr_spill_count of the code object; lane_geometry keeps to them): score
+// only TD <= 8; one-byte words TD <= 4; two-byte words TD <= 2; four-byte words TD <= 2 at NWC = 4
+template <int NWC, int TD, int CB>
+constexpr bool lane_variant_ok() {
+    return CB == 0 || (CB == 1 && TD <= 4) || (CB == 2 && TD <= 2) || (CB == 4 && TD <= 2 && NWC == 4);
 }
 
-void launch_fill_lane(hipStream_t s, const FillArgs& p) {
-    switch (p.cols_per_lane) {
-        case 1: launch_lane_td<1>(s, p); break;
-        case 2: launch_lane_td<2>(s, p); break;
-        case 4: launch_lane_td<4>(s, p); break;
-        default: launch_lane_td<8>(s, p); break;
+template <int TD, int CB>
+static void launch_lane_td(hipStream_t s, const FillArgs& p) {
+    if (p.nwc == 4) {
+        if constexpr (lane_variant_ok<4, TD, CB>()) launch_lane_one<4, TD, CB>(s, p);
+    } else {
+        if constexpr (lane_variant_ok<8, TD, CB>()) launch_lane_one<8, TD, CB>(s, p);
     }
+}
+
+template <int CB>
+static void launch_lane_cb(hipStream_t s, const FillArgs& p) {
+    switch (p.cols_per_lane) {
+        case 1: launch_lane_td<1, CB>(s, p); break;
+        case 2: launch_lane_td<2, CB>(s, p); break;
+        case 4: launch_lane_td<4, CB>(s, p); break;
+        default: launch_lane_td<8, CB>(s, p); break;
+    }
+}
+
+void launch_fill_lane(hipStream_t s, const FillArgs& p, int CB) {
+    if (p.tb == nullptr) launch_lane_cb<0>(s, p);
+    else if (CB == 1) launch_lane_cb<1>(s, p);
+    else if (CB == 2) launch_lane_cb<2>(s, p);
+    else launch_lane_cb<4>(s, p);
 }
 
 }  // namespace ga

@@ -90,3 +90,76 @@ def test_lane_sentinel_unequal(monkeypatch, m, n):
     s1, s2 = splitmix_seq(m, m + 1, "dna"), splitmix_seq(n, n + 2, "dna")
     got, cmat, goc = _fill(monkeypatch, 2, 4, s1, s2, SCORING)
     assert got == _oracle_cost(s1, s2, cmat, goc)
+
+
+# ---------------------------------------------------------------- traceback words (ga_lane.hip LkRot)
+def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_rows=None):
+    """Fill with the lane kernel's traceback words + the walk, against the oracle's dp_array_backward
+    (globaligner.py:395-593): cost, the three alignment strings and the final random state."""
+    import random
+    from globalign_amd import _native
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    from tests.conftest import load_matrix
+    a1, a2, smat, cmat, gos, goc = transform.settings(dict(kw, seq_1=s1, seq_2=s2),
+                                                      blosum=load_matrix("BLOSUM62") if protein else None)
+    random.seed(seed)
+    mt = np.array(random.getstate()[1], dtype=np.uint32)
+    ref = core.align(a1, a2, cmat, goc, mt)
+    _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
+    tables = _native.CostTables(cmat2, goc2)
+    monkeypatch.setenv("GA_FILL_MODE", "lane")
+    monkeypatch.setenv("GA_LANE_COLS_PER_LANE", str(td))
+    monkeypatch.setenv("GA_FILL_NWC", str(nwc))
+    if band_rows:
+        monkeypatch.setenv("GA_TB_BAND_ROWS", str(band_rows))
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(a1), tables.codes(a2), tables)
+        cost, strings, status, mt_after = eng.align(mt, a1, a2)
+        kind = eng.fill_kind()
+    finally:
+        eng.close()
+    assert kind[0] == "lane" and kind[1] == td, kind
+    assert status == 0
+    assert int(cost) == ref["cost"]
+    assert tuple(strings) == tuple(ref["strings"])
+    assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+
+
+@pytest.mark.parametrize("td", [1, 2, 4])
+@pytest.mark.parametrize("m,n", [(1, 1), (7, 300), (63, 64), (200, 2049), (1000, 1300), (2049, 700), (3000, 5000)])
+def test_lane_traceback_dna_vs_oracle(monkeypatch, td, m, n):
+    s1, s2 = splitmix_seq(m, m + 17, "dna"), splitmix_seq(n, n + 19, "dna")
+    _align_lane(monkeypatch, s1, s2, SCORING, seed=m ^ n ^ td, td=td)
+
+
+@pytest.mark.parametrize("td", [1, 2])
+@pytest.mark.parametrize("o", [10, 300])
+def test_lane_traceback_word_widths(monkeypatch, td, o):
+    """2- and 4-byte traceback words (o + 1 >= 8 / >= 128): the window rotation over 8 / 16 dwords."""
+    s1, s2 = splitmix_seq(900, 31 + o, "dna"), splitmix_seq(1700, 32 + o, "dna")
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-o, gap_extension_score=-1)
+    _align_lane(monkeypatch, s1, s2, kw, seed=o + td, td=td)
+
+
+@pytest.mark.parametrize("td,nwc", [(1, 8), (2, 8), (2, 4)])
+def test_lane_traceback_protein(monkeypatch, td, nwc):
+    s1, s2 = splitmix_seq(1500, 3, "protein"), splitmix_seq(2600, 4, "protein")
+    _align_lane(monkeypatch, s1, s2, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10), seed=td,
+                td=td, nwc=nwc, protein=True)
+
+
+@pytest.mark.parametrize("td", [1, 4])
+def test_lane_traceback_similar_pair(monkeypatch, td):
+    """A near-diagonal path through many ties (draw_two_random_seqs-like similar pair)."""
+    s1 = splitmix_seq(4000, 5, "dna")
+    s2 = s1[:1500] + "ACGT" + s1[1500:3000] + s1[3100:]
+    _align_lane(monkeypatch, s1, s2, SCORING, seed=11, td=td)
+
+
+@pytest.mark.parametrize("td", [1, 2])
+def test_lane_traceback_banded(monkeypatch, td):
+    """Banded (linear-memory) traceback refills through the lane kernel: checkpoint tops, prefix columns."""
+    s1, s2 = splitmix_seq(2049, 41, "dna"), splitmix_seq(3000, 42, "dna")
+    _align_lane(monkeypatch, s1, s2, SCORING, seed=7, td=td, band_rows=256)
