@@ -64,9 +64,10 @@ MULTI_GPU_DEFAULT = "c4"
 
 # committed profiles the roofline block is built from: PMC bytes and VALU
 # instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
-TRAFFIC_FILES = {"c3": "r02/traffic_c3.json", "c4": "r02/traffic_c4.json"}
-VALU_FILES = {"c3": "r02/valu_c3.json", "c4": "r02/valu_c4.json"}
-VALU_MIX_FILES = {"c3": "r02/valu_mix_c3.json", "c4": "r02/valu_mix_c4.json"}
+# (C3: the row-scan traceback fill fill_kernel; C4: the lane-skewed score fill fill_lane_kernel)
+TRAFFIC_FILES = {"c3": "r02/traffic_c3.json", "c4": "r02/traffic_c4_lane.json"}
+VALU_FILES = {"c3": "r02/valu_c3.json", "c4": "r02/valu_c4_lane.json"}
+VALU_MIX_FILES = {"c3": "r02/valu_mix_c3.json", "c4": "r02/valu_mix_c4_lane.json"}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
 
@@ -174,7 +175,7 @@ def golden_cost(workload):
     return json.load(open(path)).get("cost")
 
 
-def roofline(workload, wl, fill_ms, kernel="fill_kernel", per_step_ms=None):
+def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None):
     """What bounds the fill, from the committed profiles.
 
     The row-scan fill keeps M/X/Y in registers and LDS: it moves ~1 B/cell (PMC FETCH+WRITE), not the
@@ -187,7 +188,12 @@ def roofline(workload, wl, fill_ms, kernel="fill_kernel", per_step_ms=None):
     bpc = BYTES_PER_CELL_TB if wl["traceback"] else BYTES_PER_CELL
     traffic = _profile(TRAFFIC_FILES.get(workload, ""), "fill_kernel_hbm_bytes_per_launch")
     insts = _profile(VALU_FILES.get(workload, ""), "sq_insts_valu_per_launch")
+    if insts and profile_cells:
+        # a slab of a multi-GPU step: the 1-GPU launch's instructions per cell times the slab's cells
+        insts = insts * cells / profile_cells
+        traffic = traffic * cells / profile_cells if traffic else traffic
     mix = _profile(VALU_MIX_FILES.get(workload, ""))
+    kernel = (_profile(VALU_FILES.get(workload, ""), "kernel") or "fill").split("(")[0].replace("void ga::", "")
     secs = fill_ms * 1e-3
     hbm_alg = bpc * cells / secs / 1e9
     out = {"bound": "valu", "achieved": None, "peak": None, "unit": "wave64 VALU instructions/s", "frac": None,

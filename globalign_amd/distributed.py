@@ -480,8 +480,13 @@ def bench_main(args, wl, workload):
             # includes the pipeline wait for the left neighbour's first band
             "slab_fill_ms_max": fill_max,
             "slab_columns": [b - a for a, b in zip(edges, edges[1:])],
-            "roofline": bench.roofline(f"{workload}_slab{world}", dict(wl, n=max(b - a for a, b in zip(edges, edges[1:]))),
-                                       fill_max) if fill_max > 0 else None,
+            # the widest slab's fill against the VALU-issue bound, its instructions (and PMC bytes) per
+            # cell taken from the 1-GPU launch's profile (the slab's stripe width differs: an estimate)
+            "roofline": dict(bench.roofline(workload, dict(wl, n=max(b - a for a, b in zip(edges, edges[1:]))),
+                                            fill_max, profile_cells=m * n),
+                             note="per-cell SQ_INSTS_VALU / PMC bytes of the 1-GPU profile scaled to the widest slab; "
+                                  "slab fill time includes the wait for the left neighbour's first band")
+            if fill_max > 0 else None,
         }
         print(json.dumps(line), flush=True)
     dist.barrier()

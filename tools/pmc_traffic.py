@@ -13,7 +13,7 @@ def per_kernel(path):
     best = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        fam = "fill_kernel" if "fill_kernel" in name or "fill_diag_kernel" in name else \
+        fam = "fill_kernel" if any(k in name for k in ("fill_kernel", "fill_diag_kernel", "fill_lane_kernel")) else \
               "walk_kernel" if "walk_kernel" in name else None
         if fam is None:
             continue

@@ -9,7 +9,7 @@ import sys
 
 vals, name = {}, None
 for r in csv.DictReader(open(sys.argv[1])):
-    if "fill_kernel" not in r["Kernel_Name"] and "fill_diag_kernel" not in r["Kernel_Name"]:
+    if not any(k in r["Kernel_Name"] for k in ("fill_kernel", "fill_diag_kernel", "fill_lane_kernel")):
         continue
     c, v = r["Counter_Name"], float(r["Counter_Value"])
     if v >= vals.get(c, 0.0):

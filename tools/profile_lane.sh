@@ -1,0 +1,12 @@
+# round 2 (lane kernel): rocprofv3 kernel stats of the default bench line (C3 pipelined + the C4 point),
+# then FETCH_SIZE / WRITE_SIZE / SQ passes (each its own run) of one C4 fill (fill_lane_kernel)
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/prof2
+mkdir -p $O
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_default -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/stats_default.log 2>&1 || { tail -20 $O/stats_default.log; exit 1; }
+W=c4
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch_$W -o run -- python3 bench.py --workload $W --no-cpu-baseline --no-extra --steps 1 --warmup 0 > $O/fetch_$W.log 2>&1 || { tail -20 $O/fetch_$W.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write_$W -o run -- python3 bench.py --workload $W --no-cpu-baseline --no-extra --steps 1 --warmup 0 > $O/write_$W.log 2>&1 || { tail -20 $O/write_$W.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVES --kernel-trace --output-format csv -d $O/sq_$W -o run -- python3 bench.py --workload $W --no-cpu-baseline --no-extra --steps 1 --warmup 0 > $O/sq_$W.log 2>&1 || { tail -20 $O/sq_$W.log; exit 1; }
+find $O -name "*.csv" | sort

@@ -8,7 +8,7 @@ SIMD for full-rate forms (v_add/sub_u32, v_and/or, v_min_i16) when two waves sha
 peak for THIS kernel's mix is then 1024 SIMDs x 2.4 GHz / (mean SIMD cycles per op), which is
 what bench.py divides SQ_INSTS_VALU / kernel time by.
 
-    python tools/valu_mix.py <asm.s> <kernel symbol> [--json out.json]
+    python tools/valu_mix.py <asm.s> <kernel symbol> [--json out.json] [--skip-blocks-with v_cndmask]
 """
 import argparse
 import collections
@@ -46,7 +46,22 @@ def kernel_body(path, sym):
     return lines[start:end]
 
 
-def hottest_loop(body):
+def drop_blocks_with(lines, op):
+    """The loop's lines without the basic blocks (label to label) that contain `op`: the lane kernel's
+    masked steps (v_cndmask) run in 4 of ~10^5 sub-chunks, so its executed mix is the fast path's."""
+    out, block = [], []
+    for l in lines:
+        if re.match(r"^\.LBB\w+:", l) or re.match(r"^; %bb\.", l):
+            if not any(x.strip().startswith(op) for x in block):
+                out += block
+            block = []
+        block.append(l)
+    if not any(x.strip().startswith(op) for x in block):
+        out += block
+    return out
+
+
+def hottest_loop(body, skip_op=None):
     labels = {}
     for k, l in enumerate(body):
         mm = re.match(r"^(\.LBB\w+):", l)
@@ -57,7 +72,8 @@ def hottest_loop(body):
         mm = re.match(r"^\s+s_(cbranch_\w+|branch)\s+(\.LBB\w+)", l)
         if mm and mm.group(2) in labels and labels[mm.group(2)] < k:
             lo = labels[mm.group(2)]
-            ops = [x.split()[0] for x in body[lo:k + 1] if x.strip().startswith("v_")]
+            seg = body[lo:k + 1] if skip_op is None else drop_blocks_with(body[lo:k + 1], skip_op)
+            ops = [x.split()[0] for x in seg if x.strip().startswith("v_")]
             valu = [o for o in ops if not o.startswith(("v_readfirstlane", "v_readlane", "v_writelane"))]
             if best is None or len(valu) > len(best[2]):
                 best = (lo, k, valu)
@@ -69,8 +85,9 @@ def main():
     ap.add_argument("asm")
     ap.add_argument("symbol")
     ap.add_argument("--json")
+    ap.add_argument("--skip-blocks-with", default=None, help="drop basic blocks of the loop holding this op")
     a = ap.parse_args()
-    lo, hi, ops = hottest_loop(kernel_body(a.asm, a.symbol))
+    lo, hi, ops = hottest_loop(kernel_body(a.asm, a.symbol), a.skip_blocks_with)
     hist = collections.Counter(ops)
     cyc = sum(cost(o)[0] * c for o, c in hist.items())
     unmeasured = sorted({o for o in hist if not cost(o)[1]})
@@ -78,7 +95,7 @@ def main():
     out = {"symbol": a.symbol, "loop_lines": [lo, hi], "valu_ops_in_loop": len(ops),
            "simd_cycles_in_loop": cyc, "mean_simd_cycles_per_op": mean,
            "peak_valu_insts_per_s": 256 * 4 * 2.4e9 / mean, "unmeasured_forms_priced_at_v_min_i32": unmeasured,
-           "histogram": dict(hist.most_common())}
+           "skipped_blocks_with": a.skip_blocks_with, "histogram": dict(hist.most_common())}
     print(json.dumps(out, indent=1))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
