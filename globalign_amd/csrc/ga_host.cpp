@@ -343,6 +343,8 @@ struct ga_ctx {
     // buffers and events; the walk runs on its own stream beside the next fill
     struct PipeSlot {
         DevBuf tb, hand, flags, out_last, rng, ops, result;
+        // each pipelined alignment computes its own boundary (make_dp_array) into its slot
+        DevBuf GVp, GHp, top, left, bnd_row, bnd_col, meta, bscr;
         hipEvent_t f0 = nullptr, f1 = nullptr, fdone = nullptr, w0 = nullptr, w1 = nullptr;
         uint32_t* tab_pin = nullptr;  // pinned staging of the walk's table slice
         int64_t tab_cap = 0;
@@ -563,6 +565,9 @@ struct Band {
     hipStream_t stream = nullptr;
     bool skip_boundary = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // fill timing events instead of ctx->ev[0 / 1]
+    // boundary arrays instead of the context's (a pipeline slot's own make_dp_array output)
+    DevBuf *GVp = nullptr, *GHp = nullptr, *top_b = nullptr, *left = nullptr, *bnd_row = nullptr, *bnd_col = nullptr,
+           *meta = nullptr, *bscr = nullptr;
 };
 
 // Enqueue boundary + query profile + fill.  Does not synchronise.
@@ -632,11 +637,19 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     unsigned* fl = fb.as<unsigned>();
     // flags layout: [0] ticket, [1] abort
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(unsigned) * 16, st));
+    DevBuf& bGVp = bd.GVp ? *bd.GVp : c->GVp;
+    DevBuf& bGHp = bd.GHp ? *bd.GHp : c->GHp;
+    DevBuf& btop = bd.top_b ? *bd.top_b : c->top;
+    DevBuf& bleft = bd.left ? *bd.left : c->left;
+    DevBuf& brow = bd.bnd_row ? *bd.bnd_row : c->bnd_row;
+    DevBuf& bcol = bd.bnd_col ? *bd.bnd_col : c->bnd_col;
+    DevBuf& bmeta = bd.meta ? *bd.meta : c->meta;
+    DevBuf& bscr = bd.bscr ? *bd.bscr : c->bscr;
     if (!bd.band && !bd.skip_boundary)
         ga::launch_boundary(st, c->a.as<uint8_t>(), (int)m, c->b.as<uint8_t>(), (int)c->n_global,
-                            c->gh.as<int>(), c->gv.as<int>(), c->o, c->big, c->GVp.as<int>(), c->GHp.as<int>(),
-                            c->top.as<int2>(), c->left.as<int2>(), c->bnd_row.as<int>(), c->bnd_col.as<int>(),
-                            c->meta.as<int>(), c->custom, c->bscr.as<int>());
+                            c->gh.as<int>(), c->gv.as<int>(), c->o, c->big, bGVp.as<int>(), bGHp.as<int>(),
+                            btop.as<int2>(), bleft.as<int2>(), brow.as<int>(), bcol.as<int>(),
+                            bmeta.as<int>(), c->custom, bscr.as<int>());
     ga::FillArgs p{};
     p.a = c->a.as<uint8_t>() + bd.r0;
     p.ckpt = bd.ckpt;
@@ -644,12 +657,12 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.subp = c->qp.as<int>();
     p.K = c->K;
     p.b = c->b.as<uint8_t>() + c->col0;
-    p.top = (bd.top ? bd.top : c->top.as<int2>()) + c->col0;
+    p.top = (bd.top ? bd.top : btop.as<int2>()) + c->col0;
     if (c->slab && c->col0 > 0) {
         p.left = c->halo_in_ext ? c->halo_in_ext : c->halo_in.as<int2>();
         p.left_prog = c->prog_dev;  // [0]: halo_in rows
     } else {
-        p.left = c->left.as<int2>() + bd.r0;
+        p.left = bleft.as<int2>() + bd.r0;
         p.left_prog = nullptr;
     }
     p.hand = hb.as<int2>();
@@ -742,6 +755,8 @@ struct WalkBufs {
     int* result;
     hipStream_t stream;
     hipEvent_t ev0, ev1;
+    const int* bnd_row = nullptr;  // the boundary triples (nullptr: the context's)
+    const int* bnd_col = nullptr;
 };
 WalkBufs ctx_walk_bufs(ga_ctx* c) {
     return WalkBufs{c->tb.as<uint8_t>(), c->rng.as<uint32_t>(), c->ops.as<uint32_t>(), c->result.as<int>(), c->stream,
@@ -758,8 +773,8 @@ int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, 
     w.TC = c->TC;
     w.a = c->a.as<uint8_t>() + r0;
     w.b = c->b.as<uint8_t>() + c->col0;
-    w.bnd_row = c->bnd_row.as<int>() + 3 * c->col0;
-    w.bnd_col = c->bnd_col.as<int>() + 3 * r0;
+    w.bnd_row = (wb.bnd_row ? wb.bnd_row : c->bnd_row.as<int>()) + 3 * c->col0;
+    w.bnd_col = (wb.bnd_col ? wb.bnd_col : c->bnd_col.as<int>()) + 3 * r0;
     w.rng = wb.rng;
     w.nrng = (long long)ntab;
     w.m = (int)(mb >= 0 ? mb : c->m);
@@ -986,7 +1001,8 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
 
 // ---------------------------------------------------------------- pipelined repeated alignments
 // `count` alignments of the loaded pair, each from the random state the previous one left.  Three
-// slots of traceback words / hand-off edges / walk buffers; fills alternate between two fill
+// slots of boundary arrays / traceback words / hand-off edges / walk buffers (every alignment runs
+// the whole path: boundary, fill, table, walk, strings); fills alternate between two fill
 // streams, so fill k+1 starts on the CUs fill k leaves idle (C3: one fill holds 196 of 256 CUs)
 // and on those its tail frees, and walk k runs on a third stream beside them.  Walks are serial
 // (alignment k's table slice starts where alignment k-1's dispatches ended); a host thread extends
@@ -1014,12 +1030,28 @@ int pipe_setup(ga_ctx* c) {
         HIPCHK(sl.rng.ensure(sizeof(uint32_t) * per));
         HIPCHK(sl.ops.ensure(c->m + c->n + 1024));
         HIPCHK(sl.result.ensure(sizeof(int) * 16));
+        const int64_t m = c->m, na = c->n_global;
+        HIPCHK(sl.GVp.ensure(sizeof(int) * (m + 1)));
+        HIPCHK(sl.GHp.ensure(sizeof(int) * (na + 1)));
+        HIPCHK(sl.top.ensure(sizeof(int2) * (na + 1)));
+        HIPCHK(sl.left.ensure(sizeof(int2) * (m + 1)));
+        HIPCHK(sl.bnd_row.ensure(sizeof(int) * 3 * (na + 1)));
+        HIPCHK(sl.bnd_col.ensure(sizeof(int) * 3 * (m + 1)));
+        HIPCHK(sl.meta.ensure(sizeof(int) * 8));
+        HIPCHK(sl.bscr.ensure(sizeof(int) * ga::boundary_scratch_ints((int)m, (int)na)));
+        if (c->custom) {  // host-supplied boundary triples: the boundary pass reads them from the slot
+            HIPCHK(hipMemcpyAsync(sl.bnd_row.p, c->bnd_row.p, sizeof(int) * 3 * (na + 1), hipMemcpyDeviceToDevice,
+                                  c->stream));
+            HIPCHK(hipMemcpyAsync(sl.bnd_col.p, c->bnd_col.p, sizeof(int) * 3 * (m + 1), hipMemcpyDeviceToDevice,
+                                  c->stream));
+        }
     }
+    HIPCHK(hipStreamSynchronize(c->stream));
     return GA_OK;
 }
 
 // fill of an alignment into slot `slot` on stream `st`, then its cost inputs into pinned memory, then `fdone`
-int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool boundary) {
+int pipe_fill(ga_ctx* c, int slot, hipStream_t st) {
     auto& sl = c->pipe[slot];
     Band bd;
     bd.tbuf = &sl.tb;
@@ -1027,14 +1059,21 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool boundary) {
     bd.fbuf = &sl.flags;
     bd.obuf = &sl.out_last;
     bd.stream = st;
-    bd.skip_boundary = !boundary;
     bd.ev0 = sl.f0;
     bd.ev1 = sl.f1;
+    bd.GVp = &sl.GVp;
+    bd.GHp = &sl.GHp;
+    bd.top_b = &sl.top;
+    bd.left = &sl.left;
+    bd.bnd_row = &sl.bnd_row;
+    bd.bnd_col = &sl.bnd_col;
+    bd.meta = &sl.meta;
+    bd.bscr = &sl.bscr;
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
     int* pin = c->pipe_pin + 8 * slot;
     HIPCHK(hipMemcpyAsync(pin, sl.out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(pin + 4, c->meta.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(pin + 5, c->GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pin + 4, sl.meta.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(pin + 5, sl.GHp.as<int>() + c->col0 + c->n, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(pin + 6, sl.flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(sl.fdone, st));
     return GA_OK;
@@ -1046,12 +1085,9 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     if (int r = pipe_setup(c)) return r;
     const int64_t m = c->m, n = c->n, per = m + n + 1;
     hipStream_t fs[2] = {c->stream, c->fstream2};
-    // fill 0 computes the boundary; fills 1 (other stream) and 2 (after fill 0) start after it
-    if (int r = pipe_fill(c, 0, fs[0], true)) return r;
-    for (int k = 1; k < std::min(count, 3); k++) {
-        if (k == 1) HIPCHK(hipStreamWaitEvent(fs[1], c->pipe[0].f0, 0));
-        if (int r = pipe_fill(c, k, fs[k & 1], false)) return r;
-    }
+    // fills 0 and 1 on the two fill streams, fill 2 after fill 0; each computes its own boundary
+    for (int k = 0; k < std::min(count, 3); k++)
+        if (int r = pipe_fill(c, k, fs[k & 1])) return r;
     // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
     // vectors are reserved up front: the walks read earlier entries while later ones are written)
     RngTable& R = c->many_rng;
@@ -1099,7 +1135,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
         std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          c->wstream, sl.w0, sl.w1};
+                          c->wstream, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         return run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb);
     };
     int rc = start_walk(0, 0);
@@ -1109,7 +1145,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     for (int k = 0; k < count && rc == GA_OK; k++) {
         auto& sl = c->pipe[k % 3];
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          c->wstream, sl.w0, sl.w1};
+                          c->wstream, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         auto step = [&]() -> int {
             // walk k done: its dispatch count fixes where walk k+1's table slice starts
             HIPCHK(hipEventSynchronize(sl.w1));
@@ -1136,7 +1172,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             if (hipEventElapsedTime(&wms, sl.w0, sl.w1) == hipSuccess) walk_sum += wms;
             // fill k+3 into slot k's buffers (walk k has read them), after fill k+1 on its stream
             if (k + 3 < count)
-                if (int r = pipe_fill(c, k % 3, fs[(k + 1) & 1], false)) return r;
+                if (int r = pipe_fill(c, k % 3, fs[(k + 1) & 1])) return r;
             // alignment k's strings, while walk k+1 and the fills run
             WalkStart st{m, n, 0, 0, 0, 1};
             int reason = 0;
