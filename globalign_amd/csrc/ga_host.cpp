@@ -348,9 +348,10 @@ struct ga_ctx {
         hipEvent_t f0 = nullptr, f1 = nullptr, fdone = nullptr, w0 = nullptr, w1 = nullptr;
         uint32_t* tab_pin = nullptr;  // pinned staging of the walk's table slice
         int64_t tab_cap = 0;
-    } pipe[3];
-    hipStream_t wstream = nullptr, fstream2 = nullptr;
+    } pipe[5];
+    hipStream_t wstream = nullptr, fstream[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] unused: ctx->stream
     int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
+    int pipe_fills = 2, pipe_slots = 3;  // fills in flight (one stream each) and slots (fills + the walked one)
     RngTable many_rng;
     bool walk_rng_ready = false;
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
@@ -1009,14 +1010,16 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
 // the one continuous tie-break stream ahead of them.
 int pipe_setup(ga_ctx* c) {
     if (!c->wstream) HIPCHK(hipStreamCreateWithPriority(&c->wstream, hipStreamNonBlocking, c->priority));
-    if (!c->fstream2) HIPCHK(hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, c->priority));
+    for (int f = 1; f < 4; f++)
+        if (!c->fstream[f]) HIPCHK(hipStreamCreateWithPriority(&c->fstream[f], hipStreamNonBlocking, c->priority));
     if (!c->pipe_pin) {
         void* hp = nullptr;
-        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 32, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 8 * 5, hipHostMallocDefault));
         c->pipe_pin = static_cast<int*>(hp);
     }
     const int64_t per = c->m + c->n + 1;
-    for (auto& sl : c->pipe) {
+    for (int s = 0; s < c->pipe_slots; s++) {
+        auto& sl = c->pipe[s];
         for (hipEvent_t* e : {&sl.f0, &sl.f1, &sl.w0, &sl.w1})
             if (!*e) HIPCHK(hipEventCreate(e));
         if (!sl.fdone) HIPCHK(hipEventCreateWithFlags(&sl.fdone, hipEventDisableTiming));
@@ -1082,12 +1085,21 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st) {
 int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
                char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
     const double t0 = now_ms();
+    {
+        // fills in flight, one stream each (GA_PIPE_FILLS, 2..4).  Two: measured 3 and 4 no faster for
+        // C3 (196 of 256 CUs per fill), C5 (79) or C2 (40), whose walks bound the pipeline
+        int F = 2;
+        if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
+        c->pipe_fills = F;
+        c->pipe_slots = F + 1;
+    }
     if (int r = pipe_setup(c)) return r;
     const int64_t m = c->m, n = c->n, per = m + n + 1;
-    hipStream_t fs[2] = {c->stream, c->fstream2};
-    // fills 0 and 1 on the two fill streams, fill 2 after fill 0; each computes its own boundary
-    for (int k = 0; k < std::min(count, 3); k++)
-        if (int r = pipe_fill(c, k, fs[k & 1])) return r;
+    const int F = c->pipe_fills, S = c->pipe_slots;
+    hipStream_t fs[4] = {c->stream, c->fstream[1], c->fstream[2], c->fstream[3]};
+    // fill j into slot j % S on fill stream j % F; each computes its own boundary
+    for (int k = 0; k < std::min(count, S); k++)
+        if (int r = pipe_fill(c, k, fs[k % F])) return r;
     // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
     // vectors are reserved up front: the walks read earlier entries while later ones are written)
     RngTable& R = c->many_rng;
@@ -1127,7 +1139,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     });
     // walk k over its table slice [G, G + per), after fill k, on the walk stream
     auto start_walk = [&](int k, int64_t G) -> int {
-        auto& sl = c->pipe[k % 3];
+        auto& sl = c->pipe[k % S];
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return ready >= G + per; });
@@ -1143,7 +1155,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     int64_t Dmax = 0;
     float fill_sum = 0.f, walk_sum = 0.f;
     for (int k = 0; k < count && rc == GA_OK; k++) {
-        auto& sl = c->pipe[k % 3];
+        auto& sl = c->pipe[k % S];
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
                           c->wstream, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         auto step = [&]() -> int {
@@ -1163,16 +1175,16 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
                 if (int r = start_walk(k + 1, G + Dk)) return r;
             // alignment k's cost (fill k finished before walk k started) and walk time, before slot k's
             // pinned words and events are reused
-            const int* pin = c->pipe_pin + 8 * (k % 3);
+            const int* pin = c->pipe_pin + 8 * (k % S);
             if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
             cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
             float f = 0.f;
             if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
             float wms = 0.f;
             if (hipEventElapsedTime(&wms, sl.w0, sl.w1) == hipSuccess) walk_sum += wms;
-            // fill k+3 into slot k's buffers (walk k has read them), after fill k+1 on its stream
-            if (k + 3 < count)
-                if (int r = pipe_fill(c, k % 3, fs[(k + 1) & 1])) return r;
+            // fill k+S into slot k's buffers (walk k has read them), on its stream after fill k+S-F
+            if (k + S < count)
+                if (int r = pipe_fill(c, k % S, fs[(k + S) % F])) return r;
             // alignment k's strings, while walk k+1 and the fills run
             WalkStart st{m, n, 0, 0, 0, 1};
             int reason = 0;
@@ -1196,8 +1208,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     cv.notify_all();
     producer.join();
     if (rc != GA_OK) {
-        (void)hipStreamSynchronize(fs[0]);
-        (void)hipStreamSynchronize(fs[1]);
+        for (int f = 0; f < F; f++) (void)hipStreamSynchronize(fs[f]);
         (void)hipStreamSynchronize(c->wstream);
         return rc;
     }
@@ -1285,14 +1296,17 @@ void ga_ctx_destroy(ga_ctx* c) {
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& sl : c->pipe) {
-        for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result}) b->release();
+        for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result, &sl.GVp, &sl.GHp,
+                          &sl.top, &sl.left, &sl.bnd_row, &sl.bnd_col, &sl.meta, &sl.bscr})
+            b->release();
         for (hipEvent_t e : {sl.f0, sl.f1, sl.fdone, sl.w0, sl.w1})
             if (e) (void)hipEventDestroy(e);
         if (sl.tab_pin) (void)hipHostFree(sl.tab_pin);
     }
     if (c->pipe_pin) (void)hipHostFree(c->pipe_pin);
     if (c->wstream) (void)hipStreamDestroy(c->wstream);
-    if (c->fstream2) (void)hipStreamDestroy(c->fstream2);
+    for (int f = 1; f < 4; f++)
+        if (c->fstream[f]) (void)hipStreamDestroy(c->fstream[f]);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_dep) (void)hipEventDestroy(c->ev_dep);
