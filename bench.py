@@ -18,6 +18,7 @@ Workloads (BASELINE.json configs, SURVEY 8d SplitMix64 inputs, resident in HBM):
   c5:           20k x 20k protein (seeds 3, 4), BLOSUM62, gap_open_score -10, full traceback.
   c2:           10k x 10k DNA, full traceback.
   c1:           1k x 1k DNA (BASELINE configs[0], the reference's CPU-runnable case).
+  c4r:          1M x 16k DNA score only: a multi-rank rehearsal shape for ranks sharing one GPU.
 
 --gpus N > 1 without a torch.distributed launcher environment starts N rank processes itself
 (torch.distributed.run, 127.0.0.1) and exits with their status; it fails if fewer than N GPUs
@@ -56,6 +57,11 @@ WORKLOADS = {
     "c4tb": dict(m=1_000_000, n=1_000_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING, golden="c4",
                  desc=f"C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}; banded "
                       "traceback (checkpointed score pass + band refills, DESIGN.md 5.5)"),
+    # multi-rank rehearsal on ONE GPU only (tools/dist_rehearsal.sh): C4's rows, 16k columns, score only, so
+    # that every rank's lane-kernel slab is resident beside the others' (not a BASELINE config)
+    "c4r": dict(m=1_000_000, n=16_384, traceback=False, alphabet="dna", seeds=(1, 2), scoring=SCORING,
+                desc=f"C4 rows x 16k columns DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, score only "
+                     "(multi-rank rehearsal on one GPU)"),
     "c5": dict(m=20_000, n=20_000, traceback=True, alphabet="protein", seeds=(3, 4), scoring=PROTEIN_SCORING,
                desc="C5: 20k x 20k protein (SplitMix64 seeds 3,4), BLOSUM62, gap_open_score -10, full traceback"),
 }
