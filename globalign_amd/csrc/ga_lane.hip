@@ -37,8 +37,7 @@ namespace ga {
 // [LK_PROD0] (ring 0, the IO wave's), so compute wave w publishes {cons(w), prod(w+1)} in one store
 enum { LK_PROD0 = 31, LK_PRODQ = 40, LK_ABORT = 41, LK_SLAB = 42 };
 constexpr int LK_CNT_BYTES = 256;
-constexpr int LK_SUB = 8;      // steps per sub-chunk
-constexpr int LK_QMIRROR = 8;  // profile slots mirrored past the ring's end (a window reads idx .. idx+4)
+constexpr int LK_QMIRROR = 16;  // profile slots mirrored past the ring's end (a window reads idx .. idx+12)
 constexpr unsigned LK_DONE = 0x7fffffffu;
 typedef unsigned lk_v2u __attribute__((ext_vector_type(2)));
 
@@ -137,10 +136,26 @@ struct LkRot {
     }
 };
 
+// compile-time loop U .. N-1 over a generic lambda (steps of a sub-chunk)
+template <int U, int N>
+struct LkUnroll {
+    template <class F>
+    __device__ __forceinline__ static void run(F& f) {
+        f(std::integral_constant<int, U>{});
+        LkUnroll<U + 1, N>::run(f);
+    }
+};
+template <int N>
+struct LkUnroll<N, N> {
+    template <class F>
+    __device__ __forceinline__ static void run(F&) {}
+};
+
 // DBG: per stripe {start, end (s_memrealtime), cycles waiting for edges / profile / ring space,
 // total cycles, HW_ID} into p.dbg (tools/lane_stamps.py)
-// CB > 0: traceback words (CB bytes per cell) into p.tb in fill_kernel's aligned layout
-template <int NWC, int TD, int CB, bool DBG>
+// CB > 0: traceback words (CB bytes per cell) into p.tb in fill_kernel's aligned layout; SUB: steps per
+// sub-chunk (8 or 16: the edge / profile reads, the publish and the waits are paid once per SUB steps)
+template <int NWC, int TD, int CB, int SUB, bool DBG>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -165,7 +180,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     // 16-step windows (pairs of sub-chunks); with traceback words the last aligned word
     // (ceil(m/16) - 1) leaves lanes 48..63 at window ceil(m/16) + 3 (LkRot)
     const int tca = (m + 15) / 16;
-    const int npairs = CB > 0 ? tca + 4 : (nsteps + 2 * LK_SUB - 1) / (2 * LK_SUB);
+    const int nwin = CB > 0 ? tca + 4 : (nsteps + 15) / 16;
     const int nlive = min(NWC, p.nstripes - g * NWC);
 
     if (w == NWC) {
@@ -349,75 +364,78 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         if (DBG && t0) wcyc[kind] += __builtin_amdgcn_s_memtime() - t0;
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
-    // sub-chunk 0: lane 0's rows 1..8 (slots 0..7), the lanes' profile windows
-    int4 A[4], B[4];
-    uint32_t qA[TD][2], qB[TD][2];
-    wait_ge(prod_in, 0, avail, LK_SUB, 0);
+    // sub-chunk 0: lane 0's rows 1..SUB (slots 0..SUB-1), the lanes' profile windows
+    constexpr int NE = SUB / 2;  // int4 edge registers per sub-chunk: (H', h1') of two rows each
+    constexpr int NQ = SUB / 4;  // profile dwords per column per sub-chunk: four rows each
+    int4 A[NE], B[NE];
+    uint32_t qA[TD][NQ], qB[TD][NQ];
+    wait_ge(prod_in, 0, avail, SUB, 0);
 #pragma unroll
-    for (int k = 0; k < 4; k++) A[k] = reinterpret_cast<const int4*>(rin)[k];
-    wait_ge(&cnt[LK_PRODQ], 0, qavail, LK_SUB, 1);
+    for (int k = 0; k < NE; k++) A[k] = reinterpret_cast<const int4*>(rin)[k];
+    wait_ge(&cnt[LK_PRODQ], 0, qavail, SUB, 1);
     {
         const unsigned idx = (unsigned)(-lane) & qmask;
 #pragma unroll
-        for (int k = 0; k < TD; k++) {
-            qA[k][0] = pq[qb[k] + idx];
-            qA[k][1] = pq[qb[k] + idx + 4];
-        }
+        for (int k = 0; k < TD; k++)
+#pragma unroll
+            for (int d = 0; d < NQ; d++) qA[k][d] = pq[qb[k] + idx + 4 * d];
     }
     unsigned pnext = *prod_in;  // the producer's counter, read a sub-chunk before it is needed
-    unsigned long long out_mask = 0xff00000000000000ull;  // lanes 56..63: the shift registers' rows
+    // lanes 64-SUB .. 63: the shift registers' rows of a sub-chunk
+    unsigned long long out_mask = SUB == 16 ? 0xffff000000000000ull : 0xff00000000000000ull;
 
-    // one 8-step sub-chunk: steps r0 .. r0+7 from C / qc; after its first step the next sub-chunk's
-    // edges, profile windows and the producer's counter are read into Nx / qx / pnext (they land while
-    // steps 1..7 run); then lanes 56..63 store lane 63's eight rows and lane 0 publishes
-    // {cons(w) = r0 + 16, prod(w + 1)} in one 8-byte store
-    auto sub_chunk = [&](int r0, int4 (&C)[4], int4 (&Nx)[4], uint32_t (&qc)[TD][2], uint32_t (&qx)[TD][2], auto HALF) {
-        constexpr int HB = decltype(HALF)::value * LK_SUB;  // the sub-chunk's first step in its 16-step window
+    // one SUB-step sub-chunk: steps r0 .. r0+SUB-1 from C / qc; after its first step the next
+    // sub-chunk's edges, profile windows and the producer's counter are read into Nx / qx / pnext (they
+    // land while the other steps run); then lanes 64-SUB..63 store lane 63's SUB rows and lane 0
+    // publishes {cons(w) = r0 + 2 SUB, prod(w + 1)} in one 8-byte store
+    auto sub_chunk = [&](int r0, int4 (&C)[NE], int4 (&Nx)[NE], uint32_t (&qc)[TD][NQ], uint32_t (&qx)[TD][NQ],
+                         auto HALF) {
+        constexpr int HB = decltype(HALF)::value * SUB;  // the sub-chunk's first step in its 16-step window
         avail = sgpr_u(max(avail, pnext));
-        if ((int)avail < r0 + 2 * LK_SUB) wait_ge(prod_in, 0, avail, r0 + 2 * LK_SUB, 0);
-        if ((int)qavail < r0 + 2 * LK_SUB) wait_ge(&cnt[LK_PRODQ], 0, qavail, r0 + 2 * LK_SUB, 1);
-        const int eh[8] = {C[0].x, C[0].z, C[1].x, C[1].z, C[2].x, C[2].z, C[3].x, C[3].z};
-        const int ex[8] = {C[0].y, C[0].w, C[1].y, C[1].w, C[2].y, C[2].w, C[3].y, C[3].w};
-        uint32_t qa[TD], qd[TD];  // rows r0-l+1 .. +4 and r0-l+5 .. +8 of each column
+        if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
+        if ((int)qavail < r0 + 2 * SUB) wait_ge(&cnt[LK_PRODQ], 0, qavail, r0 + 2 * SUB, 1);
+        int eh[SUB], ex[SUB];
 #pragma unroll
-        for (int k = 0; k < TD; k++) { qa[k] = qc[k][0]; qd[k] = qc[k][1]; }
+        for (int k = 0; k < NE; k++) {
+            eh[2 * k] = C[k].x; ex[2 * k] = C[k].y; eh[2 * k + 1] = C[k].z; ex[2 * k + 1] = C[k].w;
+        }
         auto loads = [&]() {
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int k = 0; k < 4; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + LK_SUB) & RMASK))[k];
-            const unsigned idx = (unsigned)(r0 + LK_SUB - lane) & qmask;
+            for (int k = 0; k < NE; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK))[k];
+            const unsigned idx = (unsigned)(r0 + SUB - lane) & qmask;
 #pragma unroll
-            for (int k = 0; k < TD; k++) {
-                qx[k][0] = pq[qb[k] + idx];
-                qx[k][1] = pq[qb[k] + idx + 4];
-            }
+            for (int k = 0; k < TD; k++)
+#pragma unroll
+                for (int d = 0; d < NQ; d++) qx[k][d] = pq[qb[k] + idx + 4 * d];
             pnext = __hip_atomic_load(prod_in, RLX, WGS);
             asm volatile("" ::: "memory");
         };
         const int row0 = r0 - lane + 1;
         const bool capl = lane == cn / TD;
-#define LK_STEP(MK, U, QQ, UU)                                                                               \
-    lane_step<TD, U, CB, HB + UU, MK>(H, Y, Xl, Hl, HLp, RH, RX, eh[UU], ex[UU], QQ, o, acc, op1, row0 + UU, \
-                                       capl && r0 + UU == tm, ck, Hm)
-        if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)LK_SUB) {
-            LK_STEP(true, 0, qa, 0);
+        auto steps = [&](auto MK) {
+            constexpr bool MASKED = decltype(MK)::value;
+            auto one = [&](auto UC) {
+                constexpr int u = decltype(UC)::value;
+                uint32_t qq[TD];
+#pragma unroll
+                for (int k = 0; k < TD; k++) qq[k] = qc[k][u >> 2];
+                lane_step<TD, u & 3, CB, (HB + u) & 15, MASKED>(H, Y, Xl, Hl, HLp, RH, RX, eh[u], ex[u], qq, o, acc,
+                                                               op1, row0 + u, capl && r0 + u == tm, ck, Hm);
+            };
+            one(std::integral_constant<int, 0>{});
             loads();
-            LK_STEP(true, 1, qa, 1); LK_STEP(true, 2, qa, 2); LK_STEP(true, 3, qa, 3);
-            LK_STEP(true, 0, qd, 4); LK_STEP(true, 1, qd, 5); LK_STEP(true, 2, qd, 6); LK_STEP(true, 3, qd, 7);
-        } else {
-            LK_STEP(false, 0, qa, 0);
-            loads();
-            LK_STEP(false, 1, qa, 1); LK_STEP(false, 2, qa, 2); LK_STEP(false, 3, qa, 3);
-            LK_STEP(false, 0, qd, 4); LK_STEP(false, 1, qd, 5); LK_STEP(false, 2, qd, 6); LK_STEP(false, 3, qd, 7);
-        }
-#undef LK_STEP
-        // lane 63 computed rows r0-62 .. r0-55; lanes 56..63 of the shift registers hold them
+            LkUnroll<1, SUB>::run(one);
+        };
+        if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB) steps(std::true_type{});
+        else steps(std::false_type{});
+        // lane 63 computed rows r0-62 .. r0-63+SUB; lanes 64-SUB..63 of the shift registers hold them
         const int rlo = r0 - 62;
-        if ((int)outfree < rlo + LK_SUB - 1) wait_ge(cons_out, RING, outfree, rlo + LK_SUB - 1, 2);
-        const unsigned oaddr = rout_lds + (unsigned)((rlo - 57 + lane) & RMASK) * 8u;
+        if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
+        const unsigned oaddr = rout_lds + (unsigned)((rlo - 1 - (64 - SUB) + lane) & RMASK) * 8u;
         typedef int v2i_t __attribute__((ext_vector_type(2)));
         const v2i_t hx = {RH, RX};
-        const lk_v2u cp = {(unsigned)(r0 + 2 * LK_SUB), (unsigned)max(rlo + LK_SUB - 1, 0)};
+        const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
         unsigned long long saved;
         const unsigned pcl = pc_lds;            // (a generic lambda's asm operands must be its own locals)
         const unsigned long long om = out_mask;
@@ -433,14 +451,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             : "v"(oaddr), "v"(hx), "v"(pcl), "s"(om), "v"(cp)
             : "memory");
     };
-    // whole 16-step windows (steps past row m compute garbage nobody reads)
-    for (int pr = 0; pr < npairs; pr++) {
-        const int r0 = __builtin_amdgcn_readfirstlane(pr * 2 * LK_SUB);
-        sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
-        sub_chunk(r0 + LK_SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
+    // traceback words: window w of 16 steps done -> aligned word w - 1 - lane/16 of every column (LkRot)
+    auto emit = [&](int win) {
         if constexpr (CB > 0) {
-            // window pr done: aligned word pr - 1 - lane/16 of every column (LkRot)
-            const int a = pr - 1 - (lane >> 4);
+            const int a = win - 1 - (lane >> 4);
             const bool st = a >= 0 && a < tca;
 #pragma unroll
             for (int k = 0; k < TD; k++) {
@@ -460,6 +474,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 }
             }
         }
+    };
+    // whole pairs of sub-chunks (steps past row m compute garbage nobody reads); with traceback
+    // words SUB = 8, so a pair is one 16-step window
+    static_assert(CB == 0 || SUB == 8, "traceback windows are two 8-step sub-chunks");
+    const int nit = (16 * nwin + 2 * SUB - 1) / (2 * SUB);
+    for (int it = 0; it < nit; it++) {
+        const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
+        sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
+        sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
+        emit(it);
     }
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
@@ -477,10 +501,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     }
 }
 
-template <int NWC, int TD, int CB, bool DBG = false>
+template <int NWC, int TD, int CB, int SUB, bool DBG = false>
 static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     if constexpr (!DBG && CB == 0)
-        if (p.dbg != nullptr) return launch_lane_one<NWC, TD, CB, true>(s, p);
+        if (p.dbg != nullptr) return launch_lane_one<NWC, TD, CB, SUB, true>(s, p);
     // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
     static const long floor_env = [] {
         const char* e = getenv("GA_FILL_LDS_FLOOR");
@@ -488,7 +512,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
-    auto* fn = fill_lane_kernel<NWC, TD, CB, DBG>;
+    auto* fn = fill_lane_kernel<NWC, TD, CB, SUB, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
 }
@@ -502,10 +526,23 @@ constexpr bool lane_variant_ok() {
 
 template <int TD, int CB>
 static void launch_lane_td(hipStream_t s, const FillArgs& p) {
+    // score only: 16-step sub-chunks (GA_LANE_SUB=8 selects 8, for tuning); traceback words: 8
+    static const int sub_env = [] {
+        const char* e = getenv("GA_LANE_SUB");
+        return e ? atoi(e) : 16;
+    }();
+    // (TD = 8 at 8 waves per workgroup spills with 16-step sub-chunks: 8)
+    constexpr bool sub16_ok4 = CB == 0, sub16_ok8 = CB == 0 && TD < 8;
     if (p.nwc == 4) {
-        if constexpr (lane_variant_ok<4, TD, CB>()) launch_lane_one<4, TD, CB>(s, p);
+        if constexpr (lane_variant_ok<4, TD, CB>()) {
+            if (sub16_ok4 && sub_env != 8) launch_lane_one<4, TD, CB, sub16_ok4 ? 16 : 8>(s, p);
+            else launch_lane_one<4, TD, CB, 8>(s, p);
+        }
     } else {
-        if constexpr (lane_variant_ok<8, TD, CB>()) launch_lane_one<8, TD, CB>(s, p);
+        if constexpr (lane_variant_ok<8, TD, CB>()) {
+            if (sub16_ok8 && sub_env != 8) launch_lane_one<8, TD, CB, sub16_ok8 ? 16 : 8>(s, p);
+            else launch_lane_one<8, TD, CB, 8>(s, p);
+        }
     }
 }
 
