@@ -408,8 +408,23 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full, int64_t ncols = -1) {
 // Returns false (row scan) when the profile table does not fit beside the rings.
 bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
     if (c->qbytes != 1 || c->K > 32) return false;
-    static const double cyc[4][2] = {{61, 105}, {89, 160}, {131, 245}, {226, 423}};  // TD = 1, 2, 4, 8
-    const int64_t cus = c->num_cu;
+    // Cycles per step per wave measured in the kernel (score only, 16-step sub-chunks; tools/lane_stamps.py,
+    // tools/exp/lane_sub.sh, tools/exp/c4_pack.sh): one wave per SIMD (4-wave workgroups) 84 / 115 / 154 /
+    // 239 at TD = 1 / 2 / 4 / 8; two waves per SIMD (8-wave workgroups) about 2.1x that per wave, the
+    // partner's issue plus the chain coupling (C4: 243 ms against 207 for 1-wave rounds).
+    static const double cyc1[4] = {84, 115, 154, 239};
+    // workgroups per CU the residency check may count on (GA_LANE_WG_PER_CU, tuning: 2 needs an LDS floor
+    // below 80 KB, GA_FILL_LDS_FLOOR)
+    static const int wpc = [] {
+        const char* e = getenv("GA_LANE_WG_PER_CU");
+        return e ? std::max(1, std::min(2, atoi(e))) : 1;
+    }();
+    const int64_t cus = c->num_cu * wpc;
+    // Rounds: with 4-wave workgroups, one per CU, more stripes than 4 per CU run in rounds of workgroups.
+    // A later round starts as the first finish, on left edges long written, so it runs uncoupled; the
+    // chain then takes R*m + skew steps at the 1-wave step cost.  Not for a slab with a right neighbour
+    // (its last stripe, in the last round, would hold the next GPU back by the earlier rounds).
+    const bool right_nb = c->col0 + c->n < c->n_global;
     int bestT = 0, bestN = 0;
     double best = 0;
     for (int ti = 0; ti < 4; ti++) {
@@ -419,17 +434,20 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
         // words, <= 2 with two- and four-byte words (four-byte: 4 waves per workgroup)
         if (tb && T > (c->CB == 1 ? 4 : 2)) continue;
         // a slab with a right neighbour hands column n on: its last stripe must be whole
-        if (c->col0 + c->n < c->n_global && ncol % (64 * T) != 0) continue;
+        if (right_nb && ncol % (64 * T) != 0) continue;
         const int64_t ns = (ncol + 64 * T - 1) / (64 * T);
-        const int nwc = c->nwc_req == 4 || c->nwc_req == 8 ? c->nwc_req : ns <= 4 * cus ? 4 : 8;
-        if (tb && c->CB == 4 && nwc == 8) continue;
-        if (ns > nwc * cus) continue;  // not every stripe resident
-        const int wps = (ns + 4 * cus - 1) / (4 * cus) > 1 ? 1 : 0;
-        const double t = ((double)c->m + 74.0 * (double)ns) * cyc[ti][wps];
-        if (!bestT || t < best) {
-            best = t;
-            bestT = T;
-            bestN = nwc;
+        for (int nwc : {4, 8}) {
+            if ((c->nwc_req == 4 || c->nwc_req == 8) && nwc != c->nwc_req) continue;
+            if (tb && c->CB == 4 && nwc == 8) continue;
+            const int64_t rounds = (ns + nwc * cus - 1) / (nwc * cus);
+            if (rounds > 1 && (nwc == 8 || right_nb || tb)) continue;  // 8-wave workgroups: all resident
+            const double step = nwc == 4 ? cyc1[ti] : 2.1 * cyc1[ti];
+            const double t = ((double)rounds * (double)c->m + 74.0 * (double)ns) * step;
+            if (!bestT || t < best) {
+                best = t;
+                bestT = T;
+                bestN = nwc;
+            }
         }
     }
     if (!bestT) return false;

@@ -64,6 +64,16 @@ def test_lane_many_workgroups(monkeypatch, td):
     assert got == _oracle_cost(s1, s2, cmat, goc)
 
 
+@pytest.mark.parametrize("td", [1, 2])
+def test_lane_rounds(monkeypatch, td):
+    """More stripes than 4-wave workgroups can hold at once (one per CU): workgroups run in ticket-ordered
+    rounds, a later round reading hand-off rows the earlier one wrote long before (the C4 schedule)."""
+    m, n = 400, 64 * td * 4 * 300 + 21
+    s1, s2 = splitmix_seq(m, 93 + td, "dna"), splitmix_seq(n, 94 + td, "dna")
+    got, cmat, goc = _fill(monkeypatch, td, 4, s1, s2, SCORING)
+    assert got == _oracle_cost(s1, s2, cmat, goc)
+
+
 @pytest.mark.parametrize("td", [2, 8])
 def test_lane_protein_blosum62(monkeypatch, td):
     s1, s2 = splitmix_seq(1200, 31, "protein"), splitmix_seq(2500, 32, "protein")
