@@ -1,5 +1,5 @@
 set -o pipefail
-# end-of-round evidence: GPU suite, bench lines for every workload, rocprofv3 summaries (tools/profile_round.sh)
+# end-of-round evidence: GPU suite, bench lines for every workload, rocprofv3 summaries (tools/exp/profile_round.sh)
 cd /root/repo
 O=gpurun_out/final
 mkdir -p $O
@@ -11,4 +11,4 @@ for W in c3 c5 c2; do
 done
 timeout -k 10 400 python -u bench.py --workload c4tb --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_c4tb.json 2>> $O/bench.err || exit 1
 timeout -k 10 200 python -u tools/fill_stamps.py 100000 100000 --tb > $O/fill_stamps_c3.json || exit 1
-bash tools/profile_round.sh
+bash tools/exp/profile_round.sh
