@@ -8,6 +8,11 @@ __global__ void chain(long long* out, int* sink, int n) {
     const int lane = threadIdx.x & 63;
     int win = (lane * 37 + 11) & 0x7fff;
     unsigned t = 0x9e3779b9u, idx = 0, L8 = 0, acc = 0;
+    if (V == 4)  // a window image in s[64:95] (the compiler is told they are clobbered)
+        asm volatile(".irp r, 64,65,66,67,68,69,70,71,72,73,74,75,76,77,78,79,80,81,82,83,84,85,86,87,88,89,90,91,92,93,94,95\n\t"
+                     "s_mov_b32 s\\r, 0x00030002\n\t.endr" ::: "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
+                     "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85",
+                     "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
     long long t0 = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < n; k++) {
         if (V == 0) {  // the walker's step: readlane, field of the entering level, tie-break bits, move
@@ -25,6 +30,18 @@ __global__ void chain(long long* out, int* sink, int n) {
         } else if (V == 1) {  // readlane -> one scalar add -> readlane
             const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)(idx & 63));
             idx += v;
+        } else if (V == 4) {  // the step with the window in SGPRs s[64:95] (two 16-bit cells per dword),
+            // read by s_movrels_b32 with M0 = dword index: no VALU -> SALU round trip on the chain
+            unsigned v;
+            asm volatile(
+                "s_lshr_b32 m0, %1, 1\n\t"
+                "s_movrels_b32 %0, s64\n\t"
+                : "=s"(v) : "s"(idx & 63u) : "m0");
+            v = (idx & 1u) ? (v >> 16) : (v & 0xffffu);
+            const unsigned long long t64 = (unsigned long long)t << 3;
+            L8 = (unsigned)(t64 >> ((v >> L8) & 63u)) & 0x18u;
+            idx += 0x080109u >> L8;
+            acc += L8;
         } else if (V == 2) {  // eight dependent scalar ops (no readlane)
             idx = ((idx >> 3) ^ t) + 1u;
             idx = (idx >> (idx & 7u)) & 0xffffu;
@@ -57,5 +74,6 @@ int main() {
     printf("readlane -> s_add -> readlane : %.1f cyc\n", run(chain<1>));
     printf("walker step, 64-bit table     : %.1f cyc\n", run(chain<3>));
     printf("8 dependent SALU ops          : %.1f cyc\n", run(chain<2>));
+    printf("walker step, SGPR window      : %.1f cyc\n", run(chain<4>));
     return 0;
 }
