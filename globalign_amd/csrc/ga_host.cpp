@@ -350,8 +350,12 @@ struct ga_ctx {
         int64_t tab_cap = 0;
     } pipe[5];
     hipStream_t wstream = nullptr, fstream[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] unused: ctx->stream
+    // CU-masked pipeline streams (GA_PIPE_WALK_CUS > 0): the walk keeps CUs of its own, the fills the rest
+    hipStream_t mwstream = nullptr, mfstream[4] = {nullptr, nullptr, nullptr, nullptr};
+    int walk_cus = -1;  // CUs reserved for the walk (0: no masks; -1: not yet set up)
     int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
     int pipe_fills = 2, pipe_slots = 3;  // fills in flight (one stream each) and slots (fills + the walked one)
+    int pipe_lane_td = 0, pipe_lane_nwc = 0;  // the pipeline's lane-kernel fill geometry (0: the row scan)
     RngTable many_rng;
     bool walk_rng_ready = false;
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
@@ -406,7 +410,8 @@ void set_stripes(ga_ctx* c, int T_req, bool tb, bool full, int64_t ncols = -1) {
 // step per wave at one / two waves per SIMD, with the kernel's per-step LDS traffic and the DPP
 // shift-register output) times the chain's length, m steps plus ~74 steps of skew per stripe.
 // Returns false (row scan) when the profile table does not fit beside the rings.
-bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
+bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T = 0, int force_N = 0,
+                   int qrows_cap = 0) {
     if (c->qbytes != 1 || c->K > 32) return false;
     // Cycles per step per wave measured in the kernel (score only, 16-step sub-chunks; tools/lane_stamps.py,
     // tools/exp/lane_sub.sh, tools/exp/c4_pack.sh): one wave per SIMD (4-wave workgroups) 84 / 115 / 154 /
@@ -429,7 +434,7 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
     double best = 0;
     for (int ti = 0; ti < 4; ti++) {
         const int T = 1 << ti;
-        if (c->lane_T_req && c->lane_T_req != T) continue;
+        if (force_T ? force_T != T : c->lane_T_req && c->lane_T_req != T) continue;
         // traceback windows (register budget, ga_lane.hip lane_variant_ok): TD <= 4 with one-byte
         // words, <= 2 with two- and four-byte words (four-byte: 4 waves per workgroup)
         if (tb && T > (c->CB == 1 ? 4 : 2)) continue;
@@ -437,7 +442,7 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
         if (right_nb && ncol % (64 * T) != 0) continue;
         const int64_t ns = (ncol + 64 * T - 1) / (64 * T);
         for (int nwc : {4, 8}) {
-            if ((c->nwc_req == 4 || c->nwc_req == 8) && nwc != c->nwc_req) continue;
+            if (force_N ? force_N != nwc : (c->nwc_req == 4 || c->nwc_req == 8) && nwc != c->nwc_req) continue;
             if (tb && c->CB == 4 && nwc == 8) continue;
             const int64_t rounds = (ns + nwc * cus - 1) / (nwc * cus);
             if (rounds > 1 && (nwc == 8 || right_nb || tb)) continue;  // 8-wave workgroups: all resident
@@ -457,7 +462,7 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb) {
         return e ? atoi(e) : 4096;
     }();
     const size_t budget = 150 * 1024;
-    int qr = std::max(256, std::min(4096, qcap));
+    int qr = std::max(256, std::min(4096, qrows_cap > 0 ? qrows_cap : qcap));
     while (qr > 256 && ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget) qr >>= 1;
     if (ga::fill_lane_lds_bytes(bestN, c->K, qr) > budget || qr < bestN * 64 + 192) return false;
     c->T = bestT;
@@ -583,6 +588,9 @@ struct Band {
     DevBuf* obuf = nullptr;     // H'(m, n) instead of ctx->out_last
     hipStream_t stream = nullptr;
     bool skip_boundary = false;
+    // a traceback fill through the lane-skewed kernel at this geometry (TD columns per lane, NWC
+    // compute waves; 0: the usual choice): the pipeline's narrow fills (align_many)
+    int lane_td = 0, lane_nwc = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // fill timing events instead of ctx->ev[0 / 1]
     // boundary arrays instead of the context's (a pipeline slot's own make_dp_array output)
     DevBuf *GVp = nullptr, *GHp = nullptr, *top_b = nullptr, *left = nullptr, *bnd_row = nullptr, *bnd_col = nullptr,
@@ -606,8 +614,10 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // score only: the lane-skewed kernel when its chain's skew (~74 steps per stripe)
     // is short against the m rows every stripe walks (measured: 1M x 125k 60 ms against 107 for the row
     // scan, C4 244 against 312; 100k x 100k, whose 782 stripes add 58k steps of skew, 13.5 against 12.6)
-    if (!full && bd.ckpt == nullptr && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
-        lane_geometry(c, n, &qrows, tb) && (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
+    if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
+        c->lane = lane_geometry(c, n, &qrows, tb, bd.lane_td, bd.lane_nwc, 2048);
+    else if (!full && bd.ckpt == nullptr && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
+             lane_geometry(c, n, &qrows, tb) && (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
         c->lane = true;
     // automatic: score-only fills of tall problems on one GPU (m >= 4 n, <= 8 stripes per CU).
     // Measured (profiles/r01/diag_sweep.txt): 1M x 125k 80 ms (TD = 1) against 107 ms for the row
@@ -1030,6 +1040,24 @@ int pipe_setup(ga_ctx* c) {
     if (!c->wstream) HIPCHK(hipStreamCreateWithPriority(&c->wstream, hipStreamNonBlocking, c->priority));
     for (int f = 1; f < 4; f++)
         if (!c->fstream[f]) HIPCHK(hipStreamCreateWithPriority(&c->fstream[f], hipStreamNonBlocking, c->priority));
+    if (c->walk_cus < 0) {
+        // The walk's LDS tile torus (128 KB) needs a CU no fill workgroup occupies.  With the walk's CUs
+        // masked out of the fill streams it never waits for one to drain, and two fills may share the
+        // other CUs (GA_PIPE_WALK_CUS, default 0: unmasked streams)
+        int wc = 0;
+        if (const char* e = getenv("GA_PIPE_WALK_CUS")) wc = std::max(0, std::min(8, atoi(e)));
+        c->walk_cus = wc;
+        if (wc > 0) {
+            const int nc = c->num_cu, words = (nc + 31) / 32;
+            std::vector<uint32_t> fm(words, 0u), wm(words, 0u);
+            for (int cu = 0; cu < nc; cu++) {
+                auto& mk = cu >= nc - wc ? wm : fm;
+                mk[cu >> 5] |= 1u << (cu & 31);
+            }
+            HIPCHK(hipExtStreamCreateWithCUMask(&c->mwstream, (uint32_t)words, wm.data()));
+            for (int f = 0; f < 4; f++) HIPCHK(hipExtStreamCreateWithCUMask(&c->mfstream[f], (uint32_t)words, fm.data()));
+        }
+    }
     if (!c->pipe_pin) {
         void* hp = nullptr;
         HIPCHK(hipHostMalloc(&hp, sizeof(int) * 8 * 5, hipHostMallocDefault));
@@ -1090,6 +1118,8 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st) {
     bd.bnd_col = &sl.bnd_col;
     bd.meta = &sl.meta;
     bd.bscr = &sl.bscr;
+    bd.lane_td = c->pipe_lane_td;
+    bd.lane_nwc = c->pipe_lane_nwc;
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
     int* pin = c->pipe_pin + 8 * slot;
     HIPCHK(hipMemcpyAsync(pin, sl.out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
@@ -1104,9 +1134,22 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
                char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
     const double t0 = now_ms();
     {
-        // fills in flight, one stream each (GA_PIPE_FILLS, 2..4).  Two: measured 3 and 4 no faster for
-        // C3 (196 of 256 CUs per fill), C5 (79) or C2 (40), whose walks bound the pipeline
-        int F = 2;
+        // Fill kernel and fills in flight.  A row-scan traceback fill of C3 holds 196 CUs
+        // at two waves per SIMD and is issue bound there: a second fill in flight only fills the CUs it
+        // leaves idle (10.4 ms per alignment in steady state), and co-resident fills gain nothing.  The
+        // lane-skewed traceback fill at 4 columns per lane runs 391 stripes in 98 one-wave-per-SIMD
+        // workgroups: a narrow, latency-bound fill (26 ms alone), three of which share the chip
+        // (8.65 ms per alignment; tools/exp/pipe_lane2.sh).  So one-byte words of long rows (K <= 32,
+        // an int8 profile) take three lane fills; the rest two row-scan fills.  GA_PIPE_MODE=row|lane
+        // and GA_PIPE_FILLS (2..4) override.
+        const char* pm = getenv("GA_PIPE_MODE");
+        bool lane = c->CB == 1 && c->qbytes == 1 && c->K <= 32 && c->m >= 32768 && c->n >= 4 * 4 * 64 * 64 &&
+                    c->diag_req != 1 && c->diag_req != 2;
+        if (pm && !strcmp(pm, "row")) lane = false;
+        if (pm && !strcmp(pm, "lane")) lane = c->qbytes == 1 && c->K <= 32;
+        c->pipe_lane_td = lane ? (c->CB == 1 ? 4 : 2) : 0;
+        c->pipe_lane_nwc = lane ? 4 : 0;
+        int F = lane ? 3 : 2;
         if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
         c->pipe_fills = F;
         c->pipe_slots = F + 1;
@@ -1115,6 +1158,24 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     const int64_t m = c->m, n = c->n, per = m + n + 1;
     const int F = c->pipe_fills, S = c->pipe_slots;
     hipStream_t fs[4] = {c->stream, c->fstream[1], c->fstream[2], c->fstream[3]};
+    hipStream_t ws = c->wstream;
+    if (c->walk_cus > 0) {
+        for (int f = 0; f < 4; f++) fs[f] = c->mfstream[f];
+        ws = c->mwstream;
+    }
+    // GA_PIPE_TRACE=<file>: per alignment, GPU times (ms from the first fill's enqueue) of fill and walk
+    // start / end and host times of the walk launches (a diagnostic of what bounds the pipeline)
+    FILE* trace = nullptr;
+    hipEvent_t origin = nullptr;
+    if (const char* tp = getenv("GA_PIPE_TRACE")) {
+        trace = fopen(tp, "a");
+        if (trace) {
+            HIPCHK(hipEventCreate(&origin));
+            HIPCHK(hipEventRecord(origin, c->stream));
+        }
+    }
+    const double h0 = now_ms();
+    double walk_launch_host = 0.0;
     // fill j into slot j % S on fill stream j % F; each computes its own boundary
     for (int k = 0; k < std::min(count, S); k++)
         if (int r = pipe_fill(c, k, fs[k % F])) return r;
@@ -1162,20 +1223,21 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return ready >= G + per; });
         }
-        HIPCHK(hipStreamWaitEvent(c->wstream, sl.fdone, 0));
+        HIPCHK(hipStreamWaitEvent(ws, sl.fdone, 0));
         std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          c->wstream, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+                          ws, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         return run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb);
     };
     int rc = start_walk(0, 0);
+    walk_launch_host = now_ms() - h0;
     int64_t G = 0;  // global dispatches consumed by the alignments before k
     int64_t Dmax = 0;
     float fill_sum = 0.f, walk_sum = 0.f;
     for (int k = 0; k < count && rc == GA_OK; k++) {
         auto& sl = c->pipe[k % S];
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          c->wstream, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+                          ws, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         auto step = [&]() -> int {
             // walk k done: its dispatch count fixes where walk k+1's table slice starts
             HIPCHK(hipEventSynchronize(sl.w1));
@@ -1183,14 +1245,24 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             HIPCHK(hipMemcpy(res, sl.result.p, sizeof(int) * 16, hipMemcpyDeviceToHost));
             const int64_t Dk = res[0];
             Dmax = std::max(Dmax, Dk);
+            if (trace) {
+                float t[4] = {0.f, 0.f, 0.f, 0.f};
+                hipEvent_t evs[4] = {sl.f0, sl.f1, sl.w0, sl.w1};
+                for (int q = 0; q < 4; q++) (void)hipEventElapsedTime(&t[q], origin, evs[q]);
+                fprintf(trace, "{\"k\": %d, \"fill0\": %.3f, \"fill1\": %.3f, \"walk0\": %.3f, \"walk1\": %.3f, "
+                        "\"walk_launch_host\": %.3f, \"walk_done_host\": %.3f, \"D\": %lld}\n", k, t[0], t[1], t[2], t[3],
+                        walk_launch_host, now_ms() - h0, (long long)Dk);
+            }
             {
                 // keep the producer an alignment's worth (and some) ahead of the next walk
                 std::lock_guard<std::mutex> lk(mu);
                 target = std::max(target, G + Dk + per + Dmax + Dmax / 8);
             }
             cv.notify_all();
-            if (k + 1 < count)
+            if (k + 1 < count) {
                 if (int r = start_walk(k + 1, G + Dk)) return r;
+                walk_launch_host = now_ms() - h0;
+            }
             // alignment k's cost (fill k finished before walk k started) and walk time, before slot k's
             // pinned words and events are reused
             const int* pin = c->pipe_pin + 8 * (k % S);
@@ -1225,9 +1297,13 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     }
     cv.notify_all();
     producer.join();
+    if (trace) {
+        fclose(trace);
+        (void)hipEventDestroy(origin);
+    }
     if (rc != GA_OK) {
         for (int f = 0; f < F; f++) (void)hipStreamSynchronize(fs[f]);
-        (void)hipStreamSynchronize(c->wstream);
+        (void)hipStreamSynchronize(ws);
         return rc;
     }
     state_after(R, G, mt_state);  // the state the last alignment leaves (random.getstate() layout)
@@ -1323,6 +1399,9 @@ void ga_ctx_destroy(ga_ctx* c) {
     }
     if (c->pipe_pin) (void)hipHostFree(c->pipe_pin);
     if (c->wstream) (void)hipStreamDestroy(c->wstream);
+    if (c->mwstream) (void)hipStreamDestroy(c->mwstream);
+    for (hipStream_t ms : c->mfstream)
+        if (ms) (void)hipStreamDestroy(ms);
     for (int f = 1; f < 4; f++)
         if (c->fstream[f]) (void)hipStreamDestroy(c->fstream[f]);
     for (auto& e : c->ev)

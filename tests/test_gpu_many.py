@@ -85,3 +85,25 @@ def test_align_many_c3_first_matches_pin():
         assert strings2 == runs[2][1] and mt3.tolist() == mt3b.tolist()
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("mode,fills", [("lane", "3"), ("lane", "2"), ("row", "2"), ("row", "4")])
+@pytest.mark.parametrize("m,n,seed,count,kw", [
+    (2500, 3100, 11, 4, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+    (1200, 1300, 12, 3, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)),
+])
+def test_align_repeated_pipe_modes(monkeypatch, mode, fills, m, n, seed, count, kw):
+    """The pipeline's fill kernels (GA_PIPE_MODE: lane-skewed narrow fills / row-scan fills) and fills in
+    flight give the chained oracle's strings, costs and final random state."""
+    import globalign_amd
+    monkeypatch.setenv("GA_PIPE_MODE", mode)
+    monkeypatch.setenv("GA_PIPE_FILLS", fills)
+    alpha = "protein" if "scoring_mat_name" in kw else "dna"
+    s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
+    ref = _chain_oracle(s1, s2, kw, seed, count)
+    random.seed(seed)
+    runs = globalign_amd.GlobalAligner(max_seq_len_prod=None, **kw).align_repeated(s1, s2, count)
+    for r, (cost, strings, _) in zip(runs, ref):
+        assert r.cost == cost
+        assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == strings
+    assert random.getstate()[1] == tuple(int(x) for x in ref[-1][2])

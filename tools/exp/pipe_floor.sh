@@ -1,0 +1,15 @@
+# round 2: pipelined C3 with two fill workgroups per CU (LDS floor 54 KB) and 2..3 fills in flight, no CU masks
+set -o pipefail
+mkdir -p gpurun_out/exp
+run() {  # tag workload env...
+  tag=$1; W=$2; shift 2
+  rm -f gpurun_out/exp/trace_${W}_$tag.jsonl
+  env GA_PIPE_TRACE=gpurun_out/exp/trace_${W}_$tag.jsonl "$@" timeout -k 10 200 python -u bench.py --workload $W --steps 20 --warmup 3 --no-cpu-baseline --no-extra > gpurun_out/exp/pf_${W}_$tag.json 2> gpurun_out/exp/pf_${W}_$tag.err || { tail -20 gpurun_out/exp/pf_${W}_$tag.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/exp/pf_${W}_$tag.json'));print('$W $tag', round(d['ms_per_step'],3), 'fill', round(d['fill_ms'],2), 'walk', round(d['walk_ms'],2), 'rng', round(d['host_tiebreak_ms'],2), d['config']['traceback_pin']['matches_oracle'])"
+}
+run f54 c3 GA_FILL_LDS_FLOOR=54000
+run f54p3 c3 GA_FILL_LDS_FLOOR=54000 GA_PIPE_FILLS=3
+run f54t2 c3 GA_FILL_LDS_FLOOR=54000 GA_COLS_PER_LANE=2 GA_FILL_NWC=4
+run f54t2p3 c3 GA_FILL_LDS_FLOOR=54000 GA_COLS_PER_LANE=2 GA_FILL_NWC=4 GA_PIPE_FILLS=3
+run t2 c3 GA_COLS_PER_LANE=2 GA_FILL_NWC=4
+run n4 c3 GA_FILL_NWC=4
