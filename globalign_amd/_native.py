@@ -261,20 +261,21 @@ class Engine:
         -> ([(cost, strings, status)] * count, mt_words_after)"""
         mt = np.ascontiguousarray(mt_words, dtype=np.uint32).copy()
         cap = self.m + self.n + 2
-        oa, om, ob = (C.create_string_buffer(cap * count) for _ in range(3))
+        # unzeroed output rows (the engine writes each alignment's first out_len[k] bytes)
+        oa, om, ob = (np.empty(cap * count, dtype=np.uint8) for _ in range(3))
         ln = np.zeros(count, dtype=np.int64)
         st = np.zeros(count, dtype=np.int32)
         cost = np.zeros(count, dtype=np.int64)
         p64, p32 = C.POINTER(C.c_int64), C.POINTER(C.c_int32)
         _check(self._L.ga_problem_align_many(self._h, int(count), mt.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                             a_chr.encode(), b_chr.encode(), oa, om, ob, cap, ln.ctypes.data_as(p64),
+                                             a_chr.encode(), b_chr.encode(), oa.ctypes.data_as(C.c_char_p),
+                                             om.ctypes.data_as(C.c_char_p), ob.ctypes.data_as(C.c_char_p), cap,
+                                             ln.ctypes.data_as(p64),
                                              st.ctypes.data_as(p32), cost.ctypes.data_as(p64)))
         out = []
-        ra, rm, rb = oa.raw, om.raw, ob.raw
         for k in range(count):
             lo, L = k * cap, int(ln[k])
-            out.append((int(cost[k]), (ra[lo:lo + L].decode(), rm[lo:lo + L].decode(), rb[lo:lo + L].decode()),
-                        int(st[k])))
+            out.append((int(cost[k]), tuple(x[lo:lo + L].tobytes().decode() for x in (oa, om, ob)), int(st[k])))
         return out, mt
 
     def timings(self):

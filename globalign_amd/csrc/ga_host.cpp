@@ -1190,7 +1190,9 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     std::mutex mu;
     std::condition_variable cv;
     int64_t ready = 0;         // entries available to the walks (under mu)
-    int64_t target = per;      // entries the producer builds up to (under mu)
+    // entries the producer builds up to (under mu): the first three alignments' worth while the first
+    // fills run (each alignment takes about (m + n) / 1.6 dispatches), then kept ahead of the walks
+    int64_t target = std::min<int64_t>((int64_t)count * per, 3 * per);
     bool quit = false;
     double rng_ms = 0.0;
     std::thread producer([&] {

@@ -7,7 +7,7 @@ template <int V>
 __global__ void chain(long long* out, int* sink, int n) {
     const int lane = threadIdx.x & 63;
     int win = (lane * 37 + 11) & 0x7fff;
-    unsigned t = 0x9e3779b9u, idx = 0, L8 = 0, acc = 0;
+    unsigned t = 0x9e3779b9u, idx = 0, L8 = 0, acc = 0, win2 = 0;
     if (V == 4)  // a window image in s[64:95] (the compiler is told they are clobbered)
         asm volatile(".irp r, 64,65,66,67,68,69,70,71,72,73,74,75,76,77,78,79,80,81,82,83,84,85,86,87,88,89,90,91,92,93,94,95\n\t"
                      "s_mov_b32 s\\r, 0x00030002\n\t.endr" ::: "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
@@ -42,6 +42,27 @@ __global__ void chain(long long* out, int* sink, int n) {
             L8 = (unsigned)(t64 >> ((v >> L8) & 63u)) & 0x18u;
             idx += 0x080109u >> L8;
             acc += L8;
+        } else if (V == 5) {  // precomputed next-state words: readlane -> one shift -> readlane (the level's
+            // field offset comes off the chain: (f >> 3) & 0x18 while the next readlane is in flight)
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)idx);
+            const unsigned f = v >> L8;
+            idx = f;
+            L8 = (f >> 3) & 0x18u;
+            acc += L8;
+        } else if (V == 6) {  // V5 plus the per-step share of the next window's precompute (8 VALU, independent)
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)idx);
+            unsigned x = (unsigned)win;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                x = __builtin_amdgcn_ubfe(t, x & 31u, 2u) | (x << 8);
+                x = __builtin_amdgcn_perm(x, (unsigned)lane, x);
+            }
+            win2 ^= x;
+            const unsigned f = v >> L8;
+            idx = f;
+            L8 = (f >> 3) & 0x18u;
+            acc += L8;
+            t = t * 3u + 1u;
         } else if (V == 2) {  // eight dependent scalar ops (no readlane)
             idx = ((idx >> 3) ^ t) + 1u;
             idx = (idx >> (idx & 7u)) & 0xffffu;
@@ -51,7 +72,7 @@ __global__ void chain(long long* out, int* sink, int n) {
     }
     long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) out[blockIdx.x] = t1 - t0;
-    sink[blockIdx.x * blockDim.x + threadIdx.x] = (int)(idx + acc);
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = (int)(idx + acc + win2);
 }
 
 template <typename F>
@@ -75,5 +96,7 @@ int main() {
     printf("walker step, 64-bit table     : %.1f cyc\n", run(chain<3>));
     printf("8 dependent SALU ops          : %.1f cyc\n", run(chain<2>));
     printf("walker step, SGPR window      : %.1f cyc\n", run(chain<4>));
+    printf("next-state words (1 SALU)     : %.1f cyc\n", run(chain<5>));
+    printf("next-state words + 8 VALU     : %.1f cyc\n", run(chain<6>));
     return 0;
 }
