@@ -70,10 +70,11 @@ MULTI_GPU_DEFAULT = "c4"
 
 # committed profiles the roofline block is built from: PMC bytes and VALU
 # instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
-# (C3: the row-scan traceback fill fill_kernel; C4: the lane-skewed score fill fill_lane_kernel)
-TRAFFIC_FILES = {"c3": "r02/traffic_c3.json", "c4": "r02/traffic_c4_lane.json"}
-VALU_FILES = {"c3": "r02/valu_c3.json", "c4": "r02/valu_c4_lane.json"}
-VALU_MIX_FILES = {"c3": "r02/valu_mix_c3.json", "c4": "r02/valu_mix_c4_lane.json"}
+# (C3: the pipeline's lane-skewed traceback fill, fill_lane_kernel<4,4,1,8>; C4: the lane-skewed
+# score fill fill_lane_kernel<4,8,0,16>)
+TRAFFIC_FILES = {"c3": "r02/traffic_c3_lane.json", "c4": "r02/traffic_c4_lane.json"}
+VALU_FILES = {"c3": "r02/valu_c3_lane.json", "c4": "r02/valu_c4_lane.json"}
+VALU_MIX_FILES = {"c3": "r02/valu_mix_c3_lane.json", "c4": "r02/valu_mix_c4_lane.json"}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
 
@@ -215,7 +216,8 @@ def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None):
             # pipelined steps: fill launches overlap (two at a time), so one launch's duration is not the
             # time the chip spends on it; the bound is the chip's VALU issue rate over the timed steps
             out["per_launch"] = {"achieved": rate, "frac": rate / peak, "kernel_ms": fill_ms,
-                                 "note": "two fill launches run at once (ga_problem_align_many)"}
+                                 "note": "several fill launches run at once (ga_problem_align_many: three "
+                                         "lane-kernel fills for C3-shaped problems, two row-scan fills otherwise)"}
             rate = insts / (per_step_ms * 1e-3)
             out["basis"] = "chip-wide: SQ_INSTS_VALU per alignment x alignments per second of the timed region"
         else:
@@ -391,8 +393,8 @@ def launch_ranks(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C4 point of the N=1 line")
