@@ -476,14 +476,21 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         }
     };
     // whole pairs of sub-chunks (steps past row m compute garbage nobody reads); with traceback
-    // words SUB = 8, so a pair is one 16-step window
-    static_assert(CB == 0 || SUB == 8, "traceback windows are two 8-step sub-chunks");
+    // words a 16-step window is a pair of 8-step sub-chunks or one 16-step sub-chunk
+    static_assert(CB == 0 || SUB == 8 || SUB == 16, "traceback windows are 16 steps");
     const int nit = (16 * nwin + 2 * SUB - 1) / (2 * SUB);
     for (int it = 0; it < nit; it++) {
         const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
-        sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
-        sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
-        emit(it);
+        if (CB > 0 && SUB == 16) {
+            sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
+            emit(2 * it);
+            sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 0>{});
+            emit(2 * it + 1);
+        } else {
+            sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
+            sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
+            emit(it);
+        }
     }
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
@@ -526,12 +533,20 @@ constexpr bool lane_variant_ok() {
 
 template <int TD, int CB>
 static void launch_lane_td(hipStream_t s, const FillArgs& p) {
-    // score only: 16-step sub-chunks (GA_LANE_SUB=8 selects 8, for tuning); traceback words: 8
+    // score only: 16-step sub-chunks (GA_LANE_SUB=8 selects 8, for tuning); traceback words: 16-step
+    // sub-chunks for one-byte words at TD <= 4 with 4 waves (202 VGPRs, no spills; the pipelined C3 fill
+    // 26.2 -> 24.9 ms, 8.85 -> 8.34 ms per alignment in steady state; GA_LANE_TB_SUB=8 selects 8), else 8
     static const int sub_env = [] {
         const char* e = getenv("GA_LANE_SUB");
         return e ? atoi(e) : 16;
     }();
+    const char* tbe = getenv("GA_LANE_TB_SUB");  // read per launch (tests switch it)
+    const int tb_sub_env = tbe ? atoi(tbe) : 16;
     // (TD = 8 at 8 waves per workgroup spills with 16-step sub-chunks: 8)
+    constexpr bool tb16 = CB == 1 && TD <= 4;
+    if constexpr (tb16) {
+        if (p.nwc == 4 && tb_sub_env == 16) return launch_lane_one<4, TD, CB, 16>(s, p);
+    }
     constexpr bool sub16_ok4 = CB == 0, sub16_ok8 = CB == 0 && TD < 8;
     if (p.nwc == 4) {
         if constexpr (lane_variant_ok<4, TD, CB>()) {

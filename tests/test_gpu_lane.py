@@ -103,7 +103,7 @@ def test_lane_sentinel_unequal(monkeypatch, m, n):
 
 
 # ---------------------------------------------------------------- traceback words (ga_lane.hip LkRot)
-def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_rows=None):
+def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_rows=None, tb_sub=None):
     """Fill with the lane kernel's traceback words + the walk, against the oracle's dp_array_backward
     (globaligner.py:395-593): cost, the three alignment strings and the final random state."""
     import random
@@ -123,6 +123,8 @@ def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_ro
     monkeypatch.setenv("GA_FILL_NWC", str(nwc))
     if band_rows:
         monkeypatch.setenv("GA_TB_BAND_ROWS", str(band_rows))
+    if tb_sub:
+        monkeypatch.setenv("GA_LANE_TB_SUB", str(tb_sub))
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -137,11 +139,13 @@ def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_ro
     assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
 
 
+@pytest.mark.parametrize("tb_sub", [8, 16])
 @pytest.mark.parametrize("td", [1, 2, 4])
 @pytest.mark.parametrize("m,n", [(1, 1), (7, 300), (63, 64), (200, 2049), (1000, 1300), (2049, 700), (3000, 5000)])
-def test_lane_traceback_dna_vs_oracle(monkeypatch, td, m, n):
+def test_lane_traceback_dna_vs_oracle(monkeypatch, td, m, n, tb_sub):
+    """One-byte words through 8-step sub-chunk pairs and 16-step sub-chunks (one window each)."""
     s1, s2 = splitmix_seq(m, m + 17, "dna"), splitmix_seq(n, n + 19, "dna")
-    _align_lane(monkeypatch, s1, s2, SCORING, seed=m ^ n ^ td, td=td)
+    _align_lane(monkeypatch, s1, s2, SCORING, seed=m ^ n ^ td, td=td, tb_sub=tb_sub)
 
 
 @pytest.mark.parametrize("td", [1, 2])
