@@ -195,6 +195,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         const int2* rout = ring + nlive * RING;
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
         unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
+        bool in_wait = false;  // the last hand-off read found the writer behind: probe one row first
         // dword row r of code c: sub'(a_r .. a_r+3, c), rows outside 1..m zero.  A lane's window
         // may start up to 3 rows above row 1 (its first sub-chunk), so rows -2..0 are written too.
         auto put_dword = [&](int r) {
@@ -233,7 +234,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             }
             if (in_next < (unsigned)m && in_sent) {
                 const unsigned cap = min(min(lds_ld(&cnt[0]) + RING, (unsigned)m), in_next + in_win);
-                if (cap > in_next) {
+                // while the writer is behind, one 8-byte probe of its next row per round trip instead of
+                // a 32-row read of mostly unwritten rows (HBM traffic of the polls)
+                bool probe_ok = true;
+                if (cap > in_next && in_wait) {
+                    const unsigned long long x = lane == 0 ? g_ld64(src + in_next + 1) : 0ull;
+                    probe_ok = __builtin_amdgcn_readfirstlane((int)(unsigned)x) != HAND_SENT;
+                }
+                if (cap > in_next && probe_ok) {
                     const unsigned r = in_next + 1 + lane;
                     const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
                     const unsigned long long ok = __ballot(e1.x != HAND_SENT);
@@ -241,6 +249,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                     // poll window: a reader waiting on the writer looks at the next 32 rows (one
                     // sc1 round trip is ~1 us, and the chain produces a row every ~40-180 ns)
                     in_win = k >= cap - in_next ? 64u : 32u;
+                    in_wait = k < cap - in_next;
                     if (k > 0) {
                         if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
                         const unsigned hi = in_next + k;
