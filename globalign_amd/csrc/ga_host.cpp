@@ -348,10 +348,13 @@ struct ga_ctx {
         hipEvent_t f0 = nullptr, f1 = nullptr, fdone = nullptr, w0 = nullptr, w1 = nullptr;
         uint32_t* tab_pin = nullptr;  // pinned staging of the walk's table slice
         int64_t tab_cap = 0;
-    } pipe[5];
+    } pipe[6];
     hipStream_t wstream = nullptr, fstream[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] unused: ctx->stream
     // CU-masked pipeline streams (GA_PIPE_WALK_CUS > 0): the walk keeps CUs of its own, the fills the rest
     hipStream_t mwstream = nullptr, mfstream[4] = {nullptr, nullptr, nullptr, nullptr};
+    // default-priority pipeline fill streams (GA_PIPE_FILL_PRIO=normal): four fills on their own pool of
+    // hardware queues, the walk stream keeping the greatest priority (it takes the next free CU)
+    hipStream_t nfstream[4] = {nullptr, nullptr, nullptr, nullptr};
     int walk_cus = -1;  // CUs reserved for the walk (0: no masks; -1: not yet set up)
     int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
     int pipe_fills = 2, pipe_slots = 3;  // fills in flight (one stream each) and slots (fills + the walked one)
@@ -1060,7 +1063,7 @@ int pipe_setup(ga_ctx* c) {
     }
     if (!c->pipe_pin) {
         void* hp = nullptr;
-        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 8 * 5, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&hp, sizeof(int) * 8 * 6, hipHostMallocDefault));
         c->pipe_pin = static_cast<int*>(hp);
     }
     const int64_t per = c->m + c->n + 1;
@@ -1152,7 +1155,11 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         int F = lane ? 3 : 2;
         if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
         c->pipe_fills = F;
-        c->pipe_slots = F + 1;
+        // slots: fill k + S reuses walk k's buffers, so the walk chain allows one alignment per
+        // (walk + fill) / S; GA_PIPE_SLOTS raises S above F + 1 (up to 6)
+        int S = F + 1;
+        if (const char* e = getenv("GA_PIPE_SLOTS")) S = std::max(F + 1, std::min(6, atoi(e)));
+        c->pipe_slots = S;
     }
     if (int r = pipe_setup(c)) return r;
     const int64_t m = c->m, n = c->n, per = m + n + 1;
@@ -1162,6 +1169,11 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     if (c->walk_cus > 0) {
         for (int f = 0; f < 4; f++) fs[f] = c->mfstream[f];
         ws = c->mwstream;
+    } else if (const char* fp = getenv("GA_PIPE_FILL_PRIO"); fp && !strcmp(fp, "normal")) {
+        for (int f = 0; f < 4; f++) {
+            if (!c->nfstream[f]) HIPCHK(hipStreamCreateWithPriority(&c->nfstream[f], hipStreamNonBlocking, 0));
+            fs[f] = c->nfstream[f];
+        }
     }
     // GA_PIPE_TRACE=<file>: per alignment, GPU times (ms from the first fill's enqueue) of fill and walk
     // start / end and host times of the walk launches (a diagnostic of what bounds the pipeline)
@@ -1404,6 +1416,8 @@ void ga_ctx_destroy(ga_ctx* c) {
     if (c->mwstream) (void)hipStreamDestroy(c->mwstream);
     for (hipStream_t ms : c->mfstream)
         if (ms) (void)hipStreamDestroy(ms);
+    for (hipStream_t ns : c->nfstream)
+        if (ns) (void)hipStreamDestroy(ns);
     for (int f = 1; f < 4; f++)
         if (c->fstream[f]) (void)hipStreamDestroy(c->fstream[f]);
     for (auto& e : c->ev)
