@@ -619,7 +619,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // scan, C4 244 against 312; 100k x 100k, whose 782 stripes add 58k steps of skew, 13.5 against 12.6)
     if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
         c->lane = lane_geometry(c, n, &qrows, tb, bd.lane_td, bd.lane_nwc, 2048);
-    else if (!full && bd.ckpt == nullptr && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
+    else if (!full && (bd.ckpt == nullptr || !tb) && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
              lane_geometry(c, n, &qrows, tb) && (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
         c->lane = true;
     // automatic: score-only fills of tall problems on one GPU (m >= 4 n, <= 8 stripes per CU).

@@ -155,7 +155,9 @@ struct LkUnroll<N, N> {
 // total cycles, HW_ID} into p.dbg (tools/lane_stamps.py)
 // CB > 0: traceback words (CB bytes per cell) into p.tb in fill_kernel's aligned layout; SUB: steps per
 // sub-chunk (8 or 16: the edge / profile reads, the publish and the waits are paid once per SUB steps)
-template <int NWC, int TD, int CB, int SUB, bool DBG>
+// CKP: the banded traceback's score pass, storing the checkpoint rows (a variant of its own: the extra
+// paths cost the plain score fill registers)
+template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -390,6 +392,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             for (int d = 0; d < NQ; d++) qA[k][d] = pq[qb[k] + idx + 4 * d];
     }
     unsigned pnext = *prod_in;  // the producer's counter, read a sub-chunk before it is needed
+    // the banded traceback's score pass: the next checkpoint row any lane may still reach
+    int next_ck = CKP ? p.ckpt_rows : 0x7fffffff;
     // lanes 64-SUB .. 63: the shift registers' rows of a sub-chunk
     unsigned long long out_mask = SUB == 16 ? 0xffff000000000000ull : 0xff00000000000000ull;
 
@@ -422,8 +426,20 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         };
         const int row0 = r0 - lane + 1;
         const bool capl = lane == cn / TD;
-        auto steps = [&](auto MK) {
+        // checkpoint row (banded traceback's score pass): the multiple of ckpt_rows
+        // (>= 16 = SUB, so at most one) among this lane's rows of the sub-chunk, and the step it falls on
+        int cku = -1;
+        int2* ckr = nullptr;
+        auto ck_find = [&]() {
+            const int top = row0 + SUB - 1, ckrow = top >= p.ckpt_rows ? top - top % p.ckpt_rows : 0;
+            if (ckrow >= row0 && ckrow >= p.ckpt_rows && ckrow < m) {
+                cku = ckrow - row0;
+                ckr = p.ckpt + (long long)(ckrow / p.ckpt_rows - 1) * (p.n + 1);
+            }
+        };
+        auto steps = [&](auto MK, auto CKV) {
             constexpr bool MASKED = decltype(MK)::value;
+            constexpr bool CKS = decltype(CKV)::value;
             auto one = [&](auto UC) {
                 constexpr int u = decltype(UC)::value;
                 uint32_t qq[TD];
@@ -431,13 +447,36 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 for (int k = 0; k < TD; k++) qq[k] = qc[k][u >> 2];
                 lane_step<TD, u & 3, CB, (HB + u) & 15, MASKED>(H, Y, Xl, Hl, HLp, RH, RX, eh[u], ex[u], qq, o, acc,
                                                                op1, row0 + u, capl && r0 + u == tm, ck, Hm);
+                if constexpr (CKS) {
+                    if (cku == u) {
+#pragma unroll
+                        for (int k = 0; k < TD; k++)
+                            if (jl + k + 1 <= p.n) ckr[jl + k + 1] = make_int2(H[k], Y[k]);
+                    }
+                }
             };
             one(std::integral_constant<int, 0>{});
             loads();
             LkUnroll<1, SUB>::run(one);
         };
-        if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB) steps(std::true_type{});
-        else steps(std::false_type{});
+        // wave-uniform: does any lane's window hold the next checkpoint row (lanes hold rows r0-62 .. r0+SUB)?
+        const bool ckw = CKP && next_ck <= r0 + SUB;
+        if (ckw) ck_find();
+        // once lane 63's next window starts past it, the following multiple
+        if (CKP && next_ck < r0 + SUB - 62) next_ck += p.ckpt_rows;
+        if constexpr (CKP) {
+            if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB) {
+                if (ckw) steps(std::true_type{}, std::true_type{});
+                else steps(std::true_type{}, std::false_type{});
+            } else if (ckw) {
+                steps(std::false_type{}, std::true_type{});
+            } else {
+                steps(std::false_type{}, std::false_type{});
+            }
+        } else {
+            if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB) steps(std::true_type{}, std::false_type{});
+            else steps(std::false_type{}, std::false_type{});
+        }
         // lane 63 computed rows r0-62 .. r0-63+SUB; lanes 64-SUB..63 of the shift registers hold them
         const int rlo = r0 - 62;
         if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
@@ -528,6 +567,14 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
+    if constexpr (CB == 0 && !DBG) {
+        if (p.ckpt != nullptr) {  // 8-step sub-chunks: with 16 the checkpoint stores spill at TD >= 4
+            auto* fc = fill_lane_kernel<NWC, TD, CB, 8, false, true>;
+            (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            return;
+        }
+    }
     auto* fn = fill_lane_kernel<NWC, TD, CB, SUB, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);

@@ -48,6 +48,14 @@ def test_banded_dna_vs_oracle(monkeypatch, m, n, bh):
     _align(monkeypatch, s1, s2, DNA, seed=m ^ n, band_rows=bh)
 
 
+@pytest.mark.parametrize("m,n,bh", [(6000, 300, 512), (9000, 640, 2048), (4096, 1024, 16)])
+def test_banded_lane_checkpoint_pass_vs_oracle(monkeypatch, m, n, bh):
+    """Tall shapes, whose score-only checkpoint pass takes the lane-skewed kernel, the band
+    refills the row scan."""
+    s1, s2 = splitmix_seq(m, m + 3, "dna"), splitmix_seq(n, n + 5, "dna")
+    _align(monkeypatch, s1, s2, DNA, seed=m ^ bh, band_rows=bh)
+
+
 @pytest.mark.parametrize("o", [10, 300])
 def test_banded_word_widths_vs_oracle(monkeypatch, o):
     """2- and 4-byte traceback words (o + 1 >= 8 / >= 128)."""

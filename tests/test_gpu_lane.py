@@ -172,8 +172,11 @@ def test_lane_traceback_similar_pair(monkeypatch, td):
     _align_lane(monkeypatch, s1, s2, SCORING, seed=11, td=td)
 
 
-@pytest.mark.parametrize("td", [1, 2])
-def test_lane_traceback_banded(monkeypatch, td):
-    """Banded (linear-memory) traceback refills through the lane kernel: checkpoint tops, prefix columns."""
+@pytest.mark.parametrize("td", [1, 2, 4])
+@pytest.mark.parametrize("band_rows", [16, 96, 256])
+def test_lane_traceback_banded(monkeypatch, td, band_rows):
+    """Banded (linear-memory) traceback through the lane kernel: its score pass stores the checkpoint rows
+    (one per lane window at most, band_rows >= 16), then lane-kernel refills from checkpoint tops over
+    prefix columns."""
     s1, s2 = splitmix_seq(2049, 41, "dna"), splitmix_seq(3000, 42, "dna")
-    _align_lane(monkeypatch, s1, s2, SCORING, seed=7, td=td, band_rows=256)
+    _align_lane(monkeypatch, s1, s2, SCORING, seed=7 + band_rows, td=td, band_rows=band_rows)
