@@ -110,6 +110,102 @@ __global__ void bench(long long* out, int* sink, int nsteps, int o) {
     sink[blockIdx.x * blockDim.x + threadIdx.x] = z;
 }
 
+// Packed 16-bit variant: two stripes per wave in the halves of each register,
+// TD columns of each; per column pair: a v_perm for the two stripes' profile halves, then the
+// recurrence in v_pk_add_i16 (clamp) / v_pk_min_i16.  Cycles per step cover 2 x TD columns.
+typedef short s2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s2v as_s2(int x) { return __builtin_bit_cast(s2v, x); }
+__device__ __forceinline__ int as_i(s2v x) { return __builtin_bit_cast(int, x); }
+template <int TD>
+struct St16 {
+    s2v H[TD], Y[TD];
+    int Xl, Hl, HLp;
+};
+template <int TD, int U>
+__device__ __forceinline__ void lstep16(St16<TD>& s, int eh, int ex, const uint32_t (&qa)[TD], const uint32_t (&qb)[TD],
+                                        s2v o2) {
+    s2v X = as_s2(__builtin_amdgcn_update_dpp(ex, s.Xl, 0x138, 0xf, 0xf, false));
+    const int HLn = __builtin_amdgcn_update_dpp(eh, s.Hl, 0x138, 0xf, 0xf, false);
+    s2v Hd = as_s2(s.HLp);
+    constexpr unsigned sel = (U & 1) ? 0x07060302u : 0x05040100u;  // the step's int16 of each stripe's dword
+#pragma unroll
+    for (int k = 0; k < TD; k++) {
+        const s2v sb = as_s2((int)__builtin_amdgcn_perm(qb[k], qa[k], sel));
+        const s2v M = __builtin_elementwise_add_sat(Hd, sb);
+        const s2v Hn = __builtin_elementwise_min(__builtin_elementwise_min(M, X), s.Y[k]);
+        const s2v Ho = __builtin_elementwise_add_sat(Hn, o2);
+        X = __builtin_elementwise_min(X, Ho);
+        s.Y[k] = __builtin_elementwise_min(s.Y[k], Ho);
+        Hd = s.H[k];
+        s.H[k] = Hn;
+    }
+    s.Xl = as_i(X);
+    s.Hl = as_i(s.H[TD - 1]);
+    s.HLp = HLn;
+}
+
+template <int TD, int MODE>
+__global__ void bench16(long long* out, int* sink, int nsteps, int o) {
+    __shared__ __attribute__((aligned(16))) int lds[8192];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    for (int k = threadIdx.x; k < 8192; k += blockDim.x) lds[k] = (k * 37) & 0x00030003;
+    __syncthreads();
+    St16<TD> s;
+#pragma unroll
+    for (int k = 0; k < TD; k++) { s.H[k] = s2v{(short)(lane + k), (short)(lane - k)}; s.Y[k] = s2v{(short)(lane + 2 * k + 1), (short)(lane + 3)}; }
+    s.Xl = lane + 3; s.Hl = lane; s.HLp = lane + 1;
+    const s2v o2 = s2v{(short)o, (short)o};
+    // profile: int16 entries, a dword = two rows; 16 steps = 8 dwords per column per stripe
+    uint32_t qa[8][TD], qb[8][TD];
+#pragma unroll
+    for (int c = 0; c < 8; c++)
+#pragma unroll
+        for (int k = 0; k < TD; k++) { qa[c][k] = 0x00010002u * ((lane + k + c) & 3); qb[c][k] = 0x00020001u * ((lane + k + 2 * c) & 3); }
+    int4 E[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) E[k] = make_int4(k, k + 1, k + 2, k + 3);
+    int acc = 0;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < nsteps; r += 16) {
+        int eh[16], ex[16];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { eh[2 * k] = E[k].x; ex[2 * k] = E[k].y; eh[2 * k + 1] = E[k].z; ex[2 * k + 1] = E[k].w; }
+        uint32_t qan[8][TD], qbn[8][TD];
+        if (MODE >= 1) {
+            const int4* e4 = reinterpret_cast<const int4*>(lds) + ((r + 16 * w) & 511);
+#pragma unroll
+            for (int k = 0; k < 8; k++) E[k] = e4[k];
+#pragma unroll
+            for (int k = 0; k < TD; k++) {
+                const int* pa = lds + 2048 + (((r - lane + 64 * k) & 1023));
+                const int* pb = lds + 4096 + (((r - lane + 64 * k + 40) & 1023));
+#pragma unroll
+                for (int c = 0; c < 8; c++) { qan[c][k] = pa[c]; qbn[c][k] = pb[c]; }
+            }
+        }
+        int oH[16];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            lstep16<TD, 0>(s, eh[2 * c + 0], ex[2 * c + 0], qa[c], qb[c], o2); oH[2 * c + 0] = s.Hl;
+            lstep16<TD, 1>(s, eh[2 * c + 1], ex[2 * c + 1], qa[c], qb[c], o2); oH[2 * c + 1] = s.Hl;
+        }
+        if (MODE >= 1) {
+#pragma unroll
+            for (int c = 0; c < 8; c++)
+#pragma unroll
+                for (int k = 0; k < TD; k++) { qa[c][k] = qan[c][k]; qb[c][k] = qbn[c][k]; }
+        }
+        acc ^= oH[5] + oH[9];
+    }
+    long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x * 16 + w] = t1 - t0;
+    int z = s.Xl + s.Hl + s.HLp + acc;
+#pragma unroll
+    for (int k = 0; k < TD; k++) z += as_i(s.H[k]) + as_i(s.Y[k]);
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = z;
+}
+
 template <typename F>
 double run(F kern, int waves, int blocks, int n) {
     long long* d; int* s;
@@ -141,7 +237,26 @@ void row(const char* name) {
     }
 }
 
+template <int TD>
+void row16() {
+    const int n = 1 << 14;
+    auto fns = std::vector<void (*)(long long*, int*, int, int)>{bench16<TD, 0>, bench16<TD, 1>};
+    const char* modes[] = {"packed block only", "packed + LDS reads"};
+    for (int v = 0; v < 2; v++) {
+        printf("TD=%d x2 %-24s", TD, modes[v]);
+        for (int w = 1; w <= 2; w++) {
+            const double c = run(fns[v], 4 * w, 256, n);
+            printf("  %d w/SIMD %6.1f cyc/step/wave (%.3f SIMD cyc/cell)", w, c, c / w / (128.0 * TD));
+        }
+        printf("\n");
+    }
+}
+
 int main() {
+    row16<1>();
+    row16<2>();
+    row16<4>();
+    row16<8>();
     row<1>("");
     row<2>("");
     row<4>("");
