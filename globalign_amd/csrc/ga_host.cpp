@@ -1503,8 +1503,9 @@ int ga_problem_align_many(ga_ctx* c, int32_t count, uint32_t* mt_state, const ch
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status || !cost_out)
         return fail(GA_E_ARG, "null argument");
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
-    // three slots of traceback words: beyond 96 GB of them, one alignment after another
-    const bool fits = (int64_t)3 * ((c->n + 63) / 64) * 64 * c->m * c->CB <= ((int64_t)96 << 30);
+    // up to four slots of traceback words (three lane fills in flight + the walked one; GA_PIPE_SLOTS may
+    // ask for more): beyond 128 GB of them, one alignment after another
+    const bool fits = (int64_t)4 * ((c->n + 63) / 64) * 64 * c->m * c->CB <= ((int64_t)128 << 30);
     if (count == 1 || band_rows(c) > 0 || !fits) {
         // one alignment, or banded tracebacks (whose band fills hold every CU): one after another
         const double t0 = now_ms();
