@@ -1177,15 +1177,19 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     }
     // GA_PIPE_TRACE=<file>: per alignment, GPU times (ms from the first fill's enqueue) of fill and walk
     // start / end and host times of the walk launches (a diagnostic of what bounds the pipeline)
-    FILE* trace = nullptr;
-    hipEvent_t origin = nullptr;
-    if (const char* tp = getenv("GA_PIPE_TRACE")) {
-        trace = fopen(tp, "a");
-        if (trace) {
-            HIPCHK(hipEventCreate(&origin));
-            HIPCHK(hipEventRecord(origin, c->stream));
+    struct PipeTrace {  // closed on every return path
+        FILE* f = nullptr;
+        hipEvent_t origin = nullptr;
+        ~PipeTrace() {
+            if (f) fclose(f);
+            if (origin) (void)hipEventDestroy(origin);
         }
-    }
+    } tr;
+    if (const char* tp = getenv("GA_PIPE_TRACE"))
+        if (hipEventCreate(&tr.origin) == hipSuccess && hipEventRecord(tr.origin, fs[0]) == hipSuccess)
+            tr.f = fopen(tp, "a");
+    FILE* const trace = tr.f;
+    const hipEvent_t origin = tr.origin;
     const double h0 = now_ms();
     double walk_launch_host = 0.0;
     // fill j into slot j % S on fill stream j % F; each computes its own boundary
@@ -1311,10 +1315,6 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     }
     cv.notify_all();
     producer.join();
-    if (trace) {
-        fclose(trace);
-        (void)hipEventDestroy(origin);
-    }
     if (rc != GA_OK) {
         for (int f = 0; f < F; f++) (void)hipStreamSynchronize(fs[f]);
         (void)hipStreamSynchronize(ws);
