@@ -1152,7 +1152,13 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         if (pm && !strcmp(pm, "lane")) lane = c->qbytes == 1 && c->K <= 32;
         c->pipe_lane_td = lane ? (c->CB == 1 ? 4 : 2) : 0;
         c->pipe_lane_nwc = lane ? 4 : 0;
-        int F = lane ? 3 : 2;
+        // Lane fills: four in flight when the process has the hardware queues for them (the fill streams
+        // and the walk stream share a priority's pool of GPU_MAX_HW_QUEUES queues; two streams on one
+        // in-order queue serialise): C3 steady state 8.34 -> 7.81 ms per alignment, walk-bound
+        // (tools/exp/pipe_queues.sh); three with HIP's default of four queues
+        const char* hq = getenv("GPU_MAX_HW_QUEUES");
+        const int queues = hq ? atoi(hq) : 4;
+        int F = lane ? (queues >= 5 ? 4 : 3) : 2;
         if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
         c->pipe_fills = F;
         // slots: fill k + S reuses walk k's buffers, so the walk chain allows one alignment per
@@ -1503,9 +1509,9 @@ int ga_problem_align_many(ga_ctx* c, int32_t count, uint32_t* mt_state, const ch
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status || !cost_out)
         return fail(GA_E_ARG, "null argument");
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
-    // up to four slots of traceback words (three lane fills in flight + the walked one; GA_PIPE_SLOTS may
-    // ask for more): beyond 128 GB of them, one alignment after another
-    const bool fits = (int64_t)4 * ((c->n + 63) / 64) * 64 * c->m * c->CB <= ((int64_t)128 << 30);
+    // up to five slots of traceback words (four lane fills in flight + the walked one; GA_PIPE_SLOTS may
+    // ask for more): beyond 160 GB of them, one alignment after another
+    const bool fits = (int64_t)5 * ((c->n + 63) / 64) * 64 * c->m * c->CB <= ((int64_t)160 << 30);
     if (count == 1 || band_rows(c) > 0 || !fits) {
         // one alignment, or banded tracebacks (whose band fills hold every CU): one after another
         const double t0 = now_ms();

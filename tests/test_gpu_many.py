@@ -87,7 +87,7 @@ def test_align_many_c3_first_matches_pin():
         eng.close()
 
 
-@pytest.mark.parametrize("mode,fills", [("lane", "3"), ("lane", "2"), ("row", "2"), ("row", "4")])
+@pytest.mark.parametrize("mode,fills", [("lane", "4"), ("lane", "3"), ("lane", "2"), ("row", "2"), ("row", "4")])
 @pytest.mark.parametrize("m,n,seed,count,kw", [
     (2500, 3100, 11, 4, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
     (1200, 1300, 12, 3, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)),
