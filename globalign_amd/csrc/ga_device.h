@@ -65,6 +65,7 @@ struct WalkArgs {
     uint32_t* ops;        // out: 2-bit levels, dispatch D at bits 30 - 2*(D & 15) of word D >> 4
     int* result;          // out: [D, i, j, reason, diagnostics...]
     unsigned* dbg;        // optional: per tile need (ti, tj, D, wait ticks) x WALK_DBG entries, or nullptr
+    int skip_corners;     // loaders leave the block's far off-diagonal tiles (offsets (3,0), (0,3), (3,1), (1,3))
 };
 
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,

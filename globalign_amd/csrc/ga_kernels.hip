@@ -1574,6 +1574,13 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                     const int sl = li + NLOAD * q, sr = sl >> 2, sc = sl & 3;
                     const int di = (ti - sr) & (TB4 - 1), dj = (tj - sc) & (TB4 - 1);
                     cand[q] = (ti - di < 0 || tj - dj < 0) ? -1 : (((ti - di) << 16) | (tj - dj));
+                    {
+                        // speculative tiles far off the diagonal are left out (walk paths run near-diagonal):
+                        // 1: offsets (3,0) (0,3) (3,1) (1,3); 2: also (2,0) (0,2); 3: also (3,2) (2,3)
+                        const int sk = w.skip_corners, ad = abs(di - dj), mx = max(di, dj);
+                        if ((sk >= 1 && mx == TB4 - 1 && ad >= 2) || (sk >= 2 && ad >= 2) || (sk >= 3 && mx == TB4 - 1 && ad >= 1))
+                            cand[q] = -1;
+                    }
                     dist[q] = di + dj;
                 }
                 const int first_q = dist[1] < dist[0] ? 1 : 0;
