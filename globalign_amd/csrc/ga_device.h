@@ -66,6 +66,7 @@ struct WalkArgs {
     int* result;          // out: [D, i, j, reason, diagnostics...]
     unsigned* dbg;        // optional: per tile need (ti, tj, D, wait ticks) x WALK_DBG entries, or nullptr
     int skip_corners;     // loaders leave the block's far off-diagonal tiles (offsets (3,0), (0,3), (3,1), (1,3))
+    int nloaders;         // loader waves: 12, 13 (+ the idle wave 12) or 14 (+ wave 8, no L2 prefetcher)
 };
 
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,

@@ -827,6 +827,11 @@ int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, 
         // 1.45 -> 1.27 ms (tools/exp/walk_skip.sh); GA_WALK_SKIP_CORNERS = 0 / 2 / 3 for none / more
         const char* e = getenv("GA_WALK_SKIP_CORNERS");
         w.skip_corners = e ? atoi(e) : 1;
+        // 14 loader waves (the L2 prefetcher's and the idle wave's too): tile waits at C3 469 -> 186 us
+        // alone, 921 -> 413 us in the pipeline, walk 6.81 -> 6.52 ms alone, C5 1.28 -> 1.15 ms
+        // (tools/exp/walk_loaders.sh); GA_WALK_LOADERS = 12 / 13 for the former roles
+        const char* nl = getenv("GA_WALK_LOADERS");
+        w.nloaders = nl ? atoi(nl) : 14;
     }
     w.ops = wb.ops;
     w.result = wb.result;

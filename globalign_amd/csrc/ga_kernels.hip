@@ -1441,10 +1441,10 @@ constexpr int WALK_DBG = 8192;  // tile-need records kept by the diagnostic walk
 
 __device__ __forceinline__ int sgpr(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Waves: 0 walker, 4 ring helper, 8 L2 prefetcher, 12 idle (the walker's SIMD runs
-// nothing busy), the other twelve load tiles (three per SIMD).
+// Waves: 0 walker, 4 ring helper, the other fourteen load tiles (WalkArgs::nloaders = 14; with 12,
+// wave 8 is an L2 prefetcher and wave 12 idles, the walker's SIMD running nothing busy).
 constexpr int WALK_WAVES = 16;
-constexpr int NLOAD = 12;
+constexpr int NLOAD_MAX = 14;  // loader waves: 12 (default), 13 (+ the idle wave), 14 (+ the prefetcher's)
 
 __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
     const int dti = (cur >> 16) - ti, dtj = (cur & 0xffff) - tj;
@@ -1458,7 +1458,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     __shared__ uint32_t opsbuf[RB / 16];
     __shared__ uint16_t lut[256];
     __shared__ uint8_t lutF[128];
-    __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD][TT];
+    __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD_MAX][TT];
     __shared__ int tag[NSLOT];
     __shared__ int rtag[4];
     __shared__ int cur_tile, walk_done, wD, ops_flushed;
@@ -1491,7 +1491,10 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     }
     __syncthreads();
 
-    if (wave == 8) {
+    // loader waves (WalkArgs::nloaders): 12, or 13 with wave 12, or 14 with wave 8 too (no prefetcher)
+    const int nload = w.nloaders >= 12 && w.nloaders <= NLOAD_MAX ? w.nloaders : 12;
+    const bool prefetch = nload < 14, idle12 = nload < 13;
+    if (wave == 8 && prefetch) {
         // ---------------- L2 prefetcher: touches the ring of tiles just beyond the loaders'
         // 4x4 block (offsets with i+j distance 4..6, each <= 4), so their HBM fetch is
         // done by the time the block reaches them.  Low priority: it shares the walker's SIMD.
@@ -1558,9 +1561,9 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
         // Before overwriting a slot the owner invalidates its tag and re-reads the current tile:
         // a tile the walker may still read (inside its 4x4 block) is never overwritten, since
         // the walker publishes its tile before it checks a tag.
-        if (wave == 12) return;
-        const int li = wave - 1 - (wave > 4) - (wave > 8) - (wave > 12);  // 0 .. NLOAD-1
-        const int nown = li < NSLOT - NLOAD ? 2 : 1;
+        if (wave == 12 && idle12) return;
+        const int li = wave - 1 - (wave > 4) - (prefetch && wave > 8) - (idle12 && wave > 12);  // 0 .. nload-1
+        const int nown = li < NSLOT - nload ? 2 : 1;
         while (!sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS))) {
             const int cur = sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS));
             bool did = false;
@@ -1571,7 +1574,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
                     if (q >= nown) break;
-                    const int sl = li + NLOAD * q, sr = sl >> 2, sc = sl & 3;
+                    const int sl = li + nload * q, sr = sl >> 2, sc = sl & 3;
                     const int di = (ti - sr) & (TB4 - 1), dj = (tj - sc) & (TB4 - 1);
                     cand[q] = (ti - di < 0 || tj - dj < 0) ? -1 : (((ti - di) << 16) | (tj - dj));
                     {
@@ -1588,7 +1591,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                     const int q = qq ^ first_q;
                     const int tg = cand[q];
                     if (tg < 0) continue;
-                    const int sl = li + NLOAD * q, tti = tg >> 16, ttj = tg & 0xffff;
+                    const int sl = li + nload * q, tti = tg >> 16, ttj = tg & 0xffff;
                     if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
                     if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_SEQ_CST, WGS);
                     if (!in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
