@@ -221,8 +221,8 @@ def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None):
             # pipelined steps: fill launches overlap (two at a time), so one launch's duration is not the
             # time the chip spends on it; the bound is the chip's VALU issue rate over the timed steps
             out["per_launch"] = {"achieved": rate, "frac": rate / peak, "kernel_ms": fill_ms,
-                                 "note": "several fill launches run at once (ga_problem_align_many: three "
-                                         "lane-kernel fills for C3-shaped problems, two row-scan fills otherwise)"}
+                                 "note": "several fill launches run at once (ga_problem_align_many: four "
+                                         "lane-kernel fills for C3-shaped problems, three row-scan fills otherwise)"}
             rate = insts / (per_step_ms * 1e-3)
             out["basis"] = "chip-wide: SQ_INSTS_VALU per alignment x alignments per second of the timed region"
         else:

@@ -1155,7 +1155,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // lane-skewed traceback fill at 4 columns per lane runs 391 stripes in 98 one-wave-per-SIMD
         // workgroups: a narrow, latency-bound fill (26 ms alone), three of which share the chip
         // (8.65 ms per alignment; tools/exp/pipe_lane2.sh).  So one-byte words of long rows (K <= 32,
-        // an int8 profile) take three lane fills; the rest two row-scan fills.  GA_PIPE_MODE=row|lane
+        // an int8 profile) take lane fills; the rest three row-scan fills.  GA_PIPE_MODE=row|lane
         // and GA_PIPE_FILLS (2..4) override.
         const char* pm = getenv("GA_PIPE_MODE");
         bool lane = c->CB == 1 && c->qbytes == 1 && c->K <= 32 && c->m >= 32768 && c->n >= 4 * 4 * 64 * 64 &&
@@ -1170,7 +1170,9 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // (tools/exp/pipe_queues.sh); three with HIP's default of four queues
         const char* hq = getenv("GPU_MAX_HW_QUEUES");
         const int queues = hq ? atoi(hq) : 4;
-        int F = lane ? (queues >= 5 ? 4 : 3) : 2;
+        // row-scan fills: three in flight (four streams with the walk's: HIP's default pool holds them);
+        // with the faster walk C5 is no longer walk-bound (1.80 -> 1.51 ms per alignment), C2 unchanged
+        int F = lane ? (queues >= 5 ? 4 : 3) : 3;
         if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
         c->pipe_fills = F;
         // slots: fill k + S reuses walk k's buffers, so the walk chain allows one alignment per
