@@ -1115,7 +1115,7 @@ int pipe_setup(ga_ctx* c) {
 }
 
 // fill of an alignment into slot `slot` on stream `st`, then its cost inputs into pinned memory, then `fdone`
-int pipe_fill(ga_ctx* c, int slot, hipStream_t st) {
+int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool row = false) {
     auto& sl = c->pipe[slot];
     Band bd;
     bd.tbuf = &sl.tb;
@@ -1133,8 +1133,8 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st) {
     bd.bnd_col = &sl.bnd_col;
     bd.meta = &sl.meta;
     bd.bscr = &sl.bscr;
-    bd.lane_td = c->pipe_lane_td;
-    bd.lane_nwc = c->pipe_lane_nwc;
+    bd.lane_td = row ? 0 : c->pipe_lane_td;
+    bd.lane_nwc = row ? 0 : c->pipe_lane_nwc;
     if (int r = enqueue_fill(c, GA_FILL_TRACEBACK, bd)) return r;
     int* pin = c->pipe_pin + 8 * slot;
     HIPCHK(hipMemcpyAsync(pin, sl.out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
@@ -1212,9 +1212,12 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     const hipEvent_t origin = tr.origin;
     const double h0 = now_ms();
     double walk_launch_host = 0.0;
+    // experiment (GA_PIPE_ROW_FIRST=r): the first r fills through the row scan (shorter latency alone)
+    int row_first = 0;
+    if (const char* e = getenv("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
     // fill j into slot j % S on fill stream j % F; each computes its own boundary
     for (int k = 0; k < std::min(count, S); k++)
-        if (int r = pipe_fill(c, k, fs[k % F])) return r;
+        if (int r = pipe_fill(c, k, fs[k % F], k < row_first)) return r;
     // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
     // vectors are reserved up front: the walks read earlier entries while later ones are written)
     RngTable& R = c->many_rng;
