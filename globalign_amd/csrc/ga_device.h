@@ -69,6 +69,18 @@ struct WalkArgs {
     int nloaders;         // loader waves: 12, 13 (+ the idle wave 12) or 14 (+ wave 8, no L2 prefetcher)
 };
 
+// Pipelined walks in one launch (walk_chain_kernel): walk k uses w[k % S] with rng = tab + G_k.
+constexpr int WALK_CHAIN_SLOTS = 6;
+struct WalkChainArgs {
+    WalkArgs w[WALK_CHAIN_SLOTS];  // per slot: words, boundary, levels, result (rng / nrng set per walk)
+    const uint32_t* tab;           // the continuous tie-break stream (pinned host memory, device address)
+    const long long* tab_ready;    // pinned: entries of tab written so far
+    unsigned* ctl;                 // pinned: [0] fills done, [1] walks done, [2] host abort, [3] wait timed out
+    long long per;                 // entries one walk may read (m + n + 1)
+    unsigned long long wait_limit; // s_memrealtime ticks (100 MHz) a walk may wait for its fill / entries
+    int count, S;
+};
+
 void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, int n, const int* gh, const int* gv,
                      int o, int big, int* GVp, int* GHp, int2* top, int2* left, int* bnd_row, int* bnd_col, int* meta,
                      bool custom, int* scratch);
@@ -76,6 +88,7 @@ int boundary_scratch_ints(int m, int n);  // ints of scratch launch_boundary nee
 void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, bool full);
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows, int tb_stage_bytes_per_wave = 0);
 void launch_walk(hipStream_t s, const WalkArgs& w);
+void launch_walk_chain(hipStream_t s, const WalkChainArgs& a);
 // traceback words of a caller-supplied (m+1) x (n+1) x 3 cell array (dp_array_backward shim)
 void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)

@@ -360,6 +360,19 @@ struct ga_ctx {
     int pipe_fills = 2, pipe_slots = 3;  // fills in flight (one stream each) and slots (fills + the walked one)
     int pipe_lane_td = 0, pipe_lane_nwc = 0;  // the pipeline's lane-kernel fill geometry (0: the row scan)
     RngTable many_rng;
+    // chained pipeline walks (walk_chain_kernel): the tie-break stream in pinned, coherent host memory
+    // and the control words {fills done, walks done, abort, timed out, entries written (8 B at [4])}
+    uint32_t* chain_tab = nullptr;
+    int64_t chain_tab_cap = 0;
+    unsigned* chain_ctl = nullptr;
+    // the chain's stream, at the LEAST priority: HIP gives each priority its own pool of hardware
+    // queues, and no other stream of the process uses this pool, so no fill can ever be queued behind
+    // the persistent chain on an in-order queue it shares (the chain waits for those fills)
+    hipStream_t cwstream = nullptr;
+    // per slot, pinned and coherent: the walk's result words and levels, written by the chain straight
+    // into host memory (a hipMemcpy would wait for a CU, and the fills hold them all)
+    uint8_t* chain_io = nullptr;
+    size_t chain_io_cap = 0;
     bool walk_rng_ready = false;
     float fill_ms = 0.f, walk_ms = 0.f, rng_ms = 0.f, call_ms = 0.f;
     bool dbg_on = false;
@@ -795,10 +808,8 @@ WalkBufs ctx_walk_bufs(ga_ctx* c) {
                     c->ev[2], c->ev[3]};
 }
 
-int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, int64_t r0 = 0, int64_t mb = -1,
-             bool vhandoff = false, bool upload_tab = true, const WalkBufs* wbp = nullptr) {
-    const WalkBufs wb = wbp ? *wbp : ctx_walk_bufs(c);
-    if (upload_tab) HIPCHK(hipMemcpyAsync(wb.rng, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+ga::WalkArgs walk_args(ga_ctx* c, int64_t ntab, const WalkStart& st, int64_t r0, int64_t mb, bool vhandoff,
+                       const WalkBufs& wb) {
     ga::WalkArgs w{};
     w.tb = wb.tb;
     w.CB = c->CB;
@@ -835,6 +846,15 @@ int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, 
     }
     w.ops = wb.ops;
     w.result = wb.result;
+    w.dbg = nullptr;
+    return w;
+}
+
+int run_walk(ga_ctx* c, const uint32_t* tab, int64_t ntab, const WalkStart& st, int64_t r0 = 0, int64_t mb = -1,
+             bool vhandoff = false, bool upload_tab = true, const WalkBufs* wbp = nullptr) {
+    const WalkBufs wb = wbp ? *wbp : ctx_walk_bufs(c);
+    if (upload_tab) HIPCHK(hipMemcpyAsync(wb.rng, tab, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    ga::WalkArgs w = walk_args(c, ntab, st, r0, mb, vhandoff, wb);
     if (c->dbg_on) {
         HIPCHK(c->wdbg.ensure(sizeof(unsigned) * 4 * 8192));
         HIPCHK(hipMemsetAsync(c->wdbg.p, 0xff, sizeof(unsigned) * 4 * 8192, wb.stream));
@@ -852,7 +872,8 @@ inline int64_t pywrap(int64_t k, int64_t L) { return k < 0 ? k + L : k; }
 // Wait for the walk; decode the levels of dispatches [st.D, D_end) into alignment columns in walk
 // order starting at (st.i, st.j) (global columns).  Returns the end state through `st` and `reason`.
 int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const char* a_chr, const char* b_chr,
-                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced);
+                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced,
+                   const uint32_t* host_ops = nullptr);
 
 int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const char* b_chr, char* oa, char* om,
                  char* ob, int64_t cap, int64_t& len, const WalkBufs* wbp = nullptr) {
@@ -868,7 +889,8 @@ int walk_segment(ga_ctx* c, WalkStart& st, int& reason, const char* a_chr, const
 // complete, so its levels are read with a plain copy instead of on its stream (which may already
 // hold the next walk).
 int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const char* a_chr, const char* b_chr,
-                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced) {
+                   char* oa, char* om, char* ob, int64_t cap, int64_t& len, const WalkBufs& wb, bool synced,
+                   const uint32_t* host_ops) {
     c->walk_waits = res[4];
     c->walk_tiles = res[5];
     c->walk_t_tile = res[6];
@@ -883,7 +905,9 @@ int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const 
     // levels are packed 2 bits per dispatch, dispatch k at bits 30 - 2*(k & 15) of u32 word k >> 4
     const int64_t w0 = D0 >> 4, w1 = (D1 + 15) >> 4;
     std::vector<uint32_t> ops((size_t)std::max<int64_t>(w1 - w0, 0));
-    if (synced) {
+    if (host_ops) {  // the levels in pinned host memory (the walk chain writes them there)
+        if (D1 > D0) std::memcpy(ops.data(), host_ops + w0, ops.size() * sizeof(uint32_t));
+    } else if (synced) {
         if (D1 > D0) HIPCHK(hipMemcpy(ops.data(), wb.ops + w0, ops.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
     } else {
         if (D1 > D0)
@@ -1145,6 +1169,243 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool row = false) {
     return GA_OK;
 }
 
+// align_many with its walks chained in one walk_chain_kernel launch.  Each walk used to
+// start after a host round trip (walk k's end seen by the host, its dispatch count read, walk k+1's
+// table slice copied and its kernel launched: 45-55 us at C2 / C5, 0.1-0.2 ms at C3), and by then a
+// queued fill workgroup could have taken the CU the walk had left (C3: a ~1 ms gap every fourth
+// walk).  Now the walks keep their CU; walk k+1 starts when walk k ends, reading the tie-break stream
+// from G_{k+1}, which the kernel sums itself, straight out of pinned host memory that the producer
+// thread fills; the host only says which fills have ended and decodes each alignment's strings.
+int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
+                char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out, double t0) {
+    const int64_t m = c->m, n = c->n, per = m + n + 1;
+    const int F = c->pipe_fills, S = c->pipe_slots;
+    if (S > ga::WALK_CHAIN_SLOTS) return fail(GA_E_ARG, "too many pipeline slots for the walk chain");
+    hipStream_t fs[4] = {c->stream, c->fstream[1], c->fstream[2], c->fstream[3]};
+    if (!c->cwstream) {
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        const char* pe = getenv("GA_CHAIN_PRIO");  // experiments: hi / normal
+        const int pr = pe && !strcmp(pe, "hi") ? hi : pe && !strcmp(pe, "normal") ? 0 : lo;
+        HIPCHK(hipStreamCreateWithPriority(&c->cwstream, hipStreamNonBlocking, pr));
+    }
+    hipStream_t ws = c->cwstream;
+    const int64_t need = (int64_t)count * per;
+    if (c->chain_tab_cap < need) {
+        if (c->chain_tab) HIPCHK(hipHostFree(c->chain_tab));
+        c->chain_tab = nullptr;
+        c->chain_tab_cap = 0;
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, sizeof(uint32_t) * need, hipHostMallocMapped | hipHostMallocCoherent));
+        c->chain_tab = static_cast<uint32_t*>(hp);
+        c->chain_tab_cap = need;
+    }
+    if (!c->chain_ctl) {
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        c->chain_ctl = static_cast<unsigned*>(hp);
+    }
+    const size_t ops_bytes = (((size_t)(m + n + 1024) + 255) / 256) * 256, io_stride = 256 + ops_bytes;
+    if (c->chain_io_cap < io_stride * S) {
+        if (c->chain_io) HIPCHK(hipHostFree(c->chain_io));
+        c->chain_io = nullptr;
+        c->chain_io_cap = 0;
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, io_stride * S, hipHostMallocMapped | hipHostMallocCoherent));
+        c->chain_io = static_cast<uint8_t*>(hp);
+        c->chain_io_cap = io_stride * S;
+    }
+    void* io_dev = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&io_dev, c->chain_io, 0));
+    auto res_host = [&](int s) { return reinterpret_cast<int*>(c->chain_io + io_stride * s); };
+    auto ops_host = [&](int s) { return reinterpret_cast<uint32_t*>(c->chain_io + io_stride * s + 256); };
+    unsigned* ctl = c->chain_ctl;
+    long long* tab_ready = reinterpret_cast<long long*>(ctl + 4);
+    std::memset(ctl, 0, 64);
+    void *tab_dev = nullptr, *ctl_dev = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&tab_dev, c->chain_tab, 0));
+    HIPCHK(hipHostGetDevicePointer(&ctl_dev, ctl, 0));
+
+    // fill 0 first (it fixes the fill geometry and so the size of every slot's traceback words), then
+    // the walks' launch, so that its workgroup has a CU before the other fills take them all, then
+    // fills 1 .. S-1; fill j goes into slot j % S on fill stream j % F (each computes its own boundary)
+    int enqueued = 0, signalled = 0;
+    if (int r = pipe_fill(c, 0, fs[0])) return r;
+    enqueued++;
+    // every slot's fill buffers at their final size now: a reallocation's hipFree while the chain runs
+    // would wait for the chain, which waits for the host
+    const size_t tb_bytes = (size_t)c->nstripes * c->T * c->TC * 1024;
+    const size_t hand_bytes = sizeof(int2) * (size_t)c->nslabs * (m + 1);
+    for (int s = 1; s < S; s++) {
+        auto& sl = c->pipe[s];
+        HIPCHK(sl.tb.ensure(tb_bytes));
+        HIPCHK(sl.hand.ensure(hand_bytes));
+        HIPCHK(sl.flags.ensure(sizeof(unsigned) * 16));
+        HIPCHK(sl.out_last.ensure(sizeof(int) * 4));
+    }
+    ga::WalkChainArgs A{};
+    for (int s = 0; s < S; s++) {
+        auto& sl = c->pipe[s];
+        const WalkBufs wb{sl.tb.as<uint8_t>(), nullptr, sl.ops.as<uint32_t>(), sl.result.as<int>(),
+                          ws, nullptr, nullptr, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+        A.w[s] = walk_args(c, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, wb);
+        A.w[s].result = reinterpret_cast<int*>(static_cast<uint8_t*>(io_dev) + io_stride * s);
+        A.w[s].ops = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(io_dev) + io_stride * s + 256);
+    }
+    A.tab = static_cast<const uint32_t*>(tab_dev);
+    A.ctl = static_cast<unsigned*>(ctl_dev);
+    A.tab_ready = reinterpret_cast<const long long*>(static_cast<unsigned*>(ctl_dev) + 4);
+    A.per = per;
+    A.wait_limit = 100ull * 1000 * 1000 * 60;  // 60 s of s_memrealtime (100 MHz)
+    A.count = count;
+    A.S = S;
+    HIPCHK(hipEventRecord(c->pipe[0].w0, ws));
+    ga::launch_walk_chain(ws, A);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->pipe[0].w1, ws));
+    for (int k = 1; k < std::min(count, S); k++) {
+        if (int r = pipe_fill(c, k, fs[k % F])) {
+            __atomic_store_n(ctl + 2, 1u, __ATOMIC_RELEASE);
+            (void)hipStreamSynchronize(ws);
+            return r;
+        }
+        enqueued++;
+    }
+    // the tie-break stream: a host thread extends it ahead of the walks, into pinned memory
+    RngTable& R = c->many_rng;
+    R.start(mt_state);
+    R.tab.reserve((size_t)need);
+    R.step_end.reserve((size_t)need + 4);
+    R.acc.reserve((size_t)18 * need + 8);
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t ready = 0;  // entries built (under mu)
+    // walk k+1 may start the moment walk k ends, anywhere in [G_k + max(m, n), G_k + m + n]: the
+    // entries are kept two alignments' worth ahead of the last walk known to have ended
+    int64_t target = std::min<int64_t>(need, 3 * per);
+    bool quit = false;
+    double rng_ms = 0.0;
+    std::thread producer([&] {
+        for (;;) {
+            int64_t want, from;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return quit || target > ready; });
+                if (quit) return;
+                want = std::min<int64_t>(target, need);
+                from = ready;
+                if (want <= ready) {
+                    target = ready;
+                    continue;
+                }
+            }
+            const double t1 = now_ms();
+            R.extend(want);
+            std::memcpy(c->chain_tab + from, R.tab.data() + from, sizeof(uint32_t) * (want - from));
+            __atomic_store_n(tab_ready, (long long)want, __ATOMIC_RELEASE);
+            rng_ms += now_ms() - t1;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                ready = want;
+            }
+            cv.notify_all();
+        }
+    });
+    auto stop = [&](int rc) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        producer.join();
+        if (rc != GA_OK) __atomic_store_n(ctl + 2, 1u, __ATOMIC_RELEASE);  // the chain exits at its next wait
+        (void)hipStreamSynchronize(ws);
+        if (rc != GA_OK)
+            for (int f = 0; f < F; f++) (void)hipStreamSynchronize(fs[f]);
+        return rc;
+    };
+    FILE* trace = nullptr;
+    if (const char* tp = getenv("GA_PIPE_TRACE")) trace = fopen(tp, "a");
+    const double h0 = now_ms();
+    int64_t G = 0;
+    float fill_sum = 0.f, walk_sum = 0.f;
+    int rc = GA_OK;
+    for (int k = 0; k < count && rc == GA_OK; k++) {
+        auto& sl = c->pipe[k % S];
+        // wait for walk k; meanwhile tell the chain which fills have ended (in order, enqueued ones only:
+        // a slot's event still holds the previous fill of that slot until the next is enqueued)
+        for (;;) {
+            while (signalled < enqueued && hipEventQuery(c->pipe[signalled % S].fdone) == hipSuccess)
+                __atomic_store_n(ctl, (unsigned)++signalled, __ATOMIC_RELEASE);
+            if ((int)__atomic_load_n(ctl + 1, __ATOMIC_ACQUIRE) > k) break;
+            if (__atomic_load_n(ctl + 3, __ATOMIC_ACQUIRE)) {
+                rc = fail(GA_E_TIMEOUT, "chained walk waited too long for its fill or tie-break entries");
+                break;
+            }
+            std::this_thread::yield();
+        }
+        if (rc != GA_OK) break;
+        int res[16];
+        std::memcpy(res, res_host(k % S), sizeof(res));
+        const int64_t Dk = res[0];
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            target = std::max(target, G + Dk + 2 * per + per / 8);
+        }
+        cv.notify_all();
+        const int* pin = c->pipe_pin + 8 * (k % S);
+        if (pin[6]) {
+            rc = fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+            break;
+        }
+        cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
+        float f = 0.f;
+        if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
+        walk_sum += res[8] / 1.0e5f;  // the walker's own time (s_memrealtime ticks, 100 MHz)
+        if (trace)
+            fprintf(trace, "{\"k\": %d, \"chain\": 1, \"fill_ms\": %.3f, \"walk_ms\": %.3f, \"walk_done_host\": %.3f, "
+                    "\"D\": %lld, \"tile_wait_us\": %.2f, \"tile_loads\": %d}\n", k, f, res[8] / 1.0e5,
+                    now_ms() - h0, (long long)Dk, res[6] / 100.0, res[11]);
+        // fill k+S into slot k's buffers (walk k has read them)
+        if (k + S < count) {
+            if (int r = pipe_fill(c, k % S, fs[(k + S) % F])) {
+                rc = r;
+                break;
+            }
+            enqueued++;
+        }
+        // alignment k's strings, while walk k+1 and the fills run
+        const WalkBufs wb{sl.tb.as<uint8_t>(), nullptr, sl.ops.as<uint32_t>(), sl.result.as<int>(),
+                          ws, nullptr, nullptr, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+        WalkStart st{m, n, 0, 0, 0, 1};
+        int reason = 0;
+        int64_t len = 0;
+        char* a_k = oa + (size_t)k * cap;
+        char* m_k = om + (size_t)k * cap;
+        char* b_k = ob + (size_t)k * cap;
+        if (int r = decode_segment(c, res, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, wb, true,
+                                   ops_host(k % S))) {
+            rc = r;
+            break;
+        }
+        if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
+                                  &tb_status[k])) {
+            rc = r;
+            break;
+        }
+        G += st.D;
+    }
+    if (trace) fclose(trace);
+    if (int r = stop(rc)) return r;
+    state_after(R, G, mt_state);  // the state the last alignment leaves (random.getstate() layout)
+    c->fill_ms = fill_sum / count;
+    c->walk_ms = walk_sum / count;
+    c->rng_ms = (float)(rng_ms / count);
+    c->call_ms = (float)(now_ms() - t0);
+    c->filled_tb = false;
+    return GA_OK;
+}
+
 int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om,
                char* ob, int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
     const double t0 = now_ms();
@@ -1182,6 +1443,17 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         c->pipe_slots = S;
     }
     if (int r = pipe_setup(c)) return r;
+    {
+        // the walks chained in one launch (align_chain) behind row-scan fills: C2 0.908 -> 0.823 ms per
+        // alignment, C5 1.522 -> 1.507.  Not behind the lane fills: C3 8.96-9.05 -> 9.47-9.55, its four
+        // narrow fills (392 workgroups for 256 CUs) running 27.4 -> 29.5 ms each beside a walk that never
+        // gives its CU back (tools/exp/chain_ab.sh).  GA_PIPE_CHAIN=1 / 0 forces it on / off.
+        const char* ch = getenv("GA_PIPE_CHAIN");
+        const bool fits = (int64_t)count * (c->m + c->n + 1) <= ((int64_t)256 << 20);  // 1 GB of entries
+        const bool on = ch ? atoi(ch) != 0 : c->pipe_lane_td == 0;
+        if (on && fits && c->walk_cus == 0 && !getenv("GA_PIPE_FILL_PRIO") && !getenv("GA_PIPE_ROW_FIRST"))
+            return align_chain(c, count, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out, t0);
+    }
     const int64_t m = c->m, n = c->n, per = m + n + 1;
     const int F = c->pipe_fills, S = c->pipe_slots;
     hipStream_t fs[4] = {c->stream, c->fstream[1], c->fstream[2], c->fstream[3]};
@@ -1438,7 +1710,11 @@ void ga_ctx_destroy(ga_ctx* c) {
         if (sl.tab_pin) (void)hipHostFree(sl.tab_pin);
     }
     if (c->pipe_pin) (void)hipHostFree(c->pipe_pin);
+    if (c->chain_tab) (void)hipHostFree(c->chain_tab);
+    if (c->chain_ctl) (void)hipHostFree(c->chain_ctl);
+    if (c->chain_io) (void)hipHostFree(c->chain_io);
     if (c->wstream) (void)hipStreamDestroy(c->wstream);
+    if (c->cwstream) (void)hipStreamDestroy(c->cwstream);
     if (c->mwstream) (void)hipStreamDestroy(c->mwstream);
     for (hipStream_t ms : c->mfstream)
         if (ms) (void)hipStreamDestroy(ms);

@@ -1451,8 +1451,14 @@ __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
     return cur >= 0 && dti >= 0 && dti < TB4 && dtj >= 0 && dtj < TB4;
 }
 
+// One walk by the whole workgroup (every wave returns from here once its role is done): the body of
+// walk_kernel, and of walk_chain_kernel once per alignment.  It initialises all of its LDS state.
 template <int CB>
-__global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
+__device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng) {
+    // the thread index through an opaque copy: in walk_chain_kernel nothing derived from it is hoisted
+    // out of the loop over walks (it would stay live in VGPRs across every role's code)
+    unsigned tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     __shared__ uint16_t torus[TP * TP];
     __shared__ __attribute__((aligned(16))) uint32_t rngbuf[RB];
     __shared__ uint32_t opsbuf[RB / 16];
@@ -1464,24 +1470,24 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     __shared__ int cur_tile, walk_done, wD, ops_flushed;
     __shared__ unsigned long long load_ticks;
     __shared__ int load_count;
-    const int lane = threadIdx.x & 63;
-    const int wave = sgpr(threadIdx.x >> 6);
+    const int lane = tid & 63;
+    const int wave = sgpr(tid >> 6);
     const int m = w.m, n = w.n, o = w.o;
-    if (threadIdx.x == 0) { load_ticks = 0; load_count = 0; }
-    if (threadIdx.x < NSLOT) tag[threadIdx.x] = -1;
-    if (threadIdx.x < 4) rtag[threadIdx.x] = -1;
+    if (tid == 0) { load_ticks = 0; load_count = 0; }
+    if (tid < NSLOT) tag[tid] = -1;
+    if (tid < 4) rtag[tid] = -1;
     // a slab walk starts at dispatch D0: the rings start at its block
-    if (threadIdx.x == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; }
-    if (CB == 1 && threadIdx.x < 256)
-        lut[threadIdx.x] = (uint16_t)cell_shifts(sets_from_code(threadIdx.x & 127u, 1, o), (threadIdx.x >> 7) != 0);
-    if (CB == 2 && threadIdx.x < 128) {
-        const int v = (int)threadIdx.x;
+    if (tid == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; }
+    if (CB == 1 && tid < 256)
+        lut[tid] = (uint16_t)cell_shifts(sets_from_code(tid & 127u, 1, o), (tid >> 7) != 0);
+    if (CB == 2 && tid < 128) {
+        const int v = (int)tid;
         lutF[v] = (uint8_t)((v == 0) | ((v <= o) << 1) | ((v >= o) << 2));
     }
-    if (CB == 2 && threadIdx.x < 256) {
+    if (CB == 2 && tid < 256) {
         // sets_from_code in terms of the flags: bit 0 the raw zM bit, bits 1-3 / 4-6 the (zero, le, ge)
         // flags of the X / Y fields, bit 7 a_i == b_j
-        const unsigned x = threadIdx.x;
+        const unsigned x = tid;
         const unsigned zM = (x & 1u) ^ 1u, zX = (x >> 1) & 1u, leX = (x >> 2) & 1u, geX = (x >> 3) & 1u;
         const unsigned zY = (x >> 4) & 1u, leY = (x >> 5) & 1u, geY = (x >> 6) & 1u;
         const unsigned S0 = zM | (zX << 1) | (zY << 2);
@@ -1535,7 +1541,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
                 const long long e0 = rl * 512 + lane * 8;
                 uint32_t* dst = rngbuf + (rl & 3) * 512 + lane * 8;
 #pragma unroll
-                for (int k = 0; k < 8; k++) dst[k] = (e0 + k < w.nrng) ? w.rng[e0 + k] : 0u;
+                for (int k = 0; k < 8; k++) dst[k] = (e0 + k < w.nrng) ? rng[e0 + k] : 0u;
                 if (lane == 0) __hip_atomic_store(&rtag[rl & 3], (int)rl, __ATOMIC_RELEASE, WGS);
                 rl++;
                 moved = true;
@@ -1853,6 +1859,96 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
     }
 }
 
+template <int CB>
+__global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
+    walk_body<CB>(w, w.rng);
+}
+
+// A slot's walk arguments, read from the kernel arguments at a run-time index (vector loads), made
+// wave-uniform field by field, so that the walk's control and addresses stay in scalar registers as
+// in walk_kernel (without it the chain's walks held them in VGPRs and loaded tiles ~2x slower)
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+    const unsigned long long x = (unsigned long long)p;
+    return (T*)(((unsigned long long)(unsigned)sgpr((int)(x >> 32)) << 32) | (unsigned)sgpr((int)x));
+}
+__device__ __forceinline__ WalkArgs uniform_walk_args(const WalkArgs& s) {
+    WalkArgs w;
+    w.tb = sgpr_ptr(s.tb);
+    w.CB = sgpr(s.CB);
+    w.TC = sgpr(s.TC);
+    w.a = sgpr_ptr(s.a);
+    w.b = sgpr_ptr(s.b);
+    w.bnd_row = sgpr_ptr(s.bnd_row);
+    w.bnd_col = sgpr_ptr(s.bnd_col);
+    w.rng = nullptr;
+    w.nrng = (long long)(((unsigned long long)(unsigned)sgpr((int)(s.nrng >> 32)) << 32) | (unsigned)sgpr((int)s.nrng));
+    w.m = sgpr(s.m);
+    w.n = sgpr(s.n);
+    w.o = sgpr(s.o);
+    w.i0 = sgpr(s.i0);
+    w.j0 = sgpr(s.j0);
+    w.L0 = sgpr(s.L0);
+    w.first0 = sgpr(s.first0);
+    w.D0 = sgpr(s.D0);
+    w.h0 = sgpr(s.h0);
+    w.handoff = sgpr(s.handoff);
+    w.vhandoff = sgpr(s.vhandoff);
+    w.maxh = sgpr(s.maxh);
+    w.ops = sgpr_ptr(s.ops);
+    w.result = sgpr_ptr(s.result);
+    w.dbg = sgpr_ptr(s.dbg);
+    w.skip_corners = sgpr(s.skip_corners);
+    w.nloaders = sgpr(s.nloaders);
+    return w;
+}
+
+// The pipelined alignments' walks, one after another in ONE launch: walk k starts as
+// soon as walk k-1 has ended, on the CU the walks keep, with no host round trip in between.  Walk k
+// reads the tie-break stream from global dispatch G_k = D_0 + ... + D_{k-1}, which only the walks
+// know.  The host raises ctl[0] (fills done, in order; every fill has ended and its words are in
+// HBM) and tab_ready (entries of the stream written); the kernel raises ctl[1] (walks done, their
+// levels and results written back) and, on a wait past wait_limit, ctl[3].  ctl[2] = 1 (host) ends it.
+template <int CB>
+__global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainArgs a) {
+    __shared__ int go;
+    __shared__ long long gnext;
+    long long G = 0;
+    for (int k = 0; k < a.count; k++) {
+        if (threadIdx.x == 0) {
+            int ok = 1;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                if (__hip_atomic_load(a.ctl + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) { ok = 0; break; }
+                if ((int)__hip_atomic_load(a.ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) > k &&
+                    __hip_atomic_load(const_cast<long long*>(a.tab_ready), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= G + a.per)
+                    break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_limit) {
+                    __hip_atomic_store(a.ctl + 3, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            go = ok;
+        }
+        __syncthreads();
+        if (!sgpr(go)) return;  // uniform: the walks' control flow and arguments stay scalar
+        __threadfence();  // acquire: the slot's traceback words and boundary, written by fill k
+        const WalkArgs w = uniform_walk_args(a.w[k % a.S]);
+        walk_body<CB>(w, a.tab + G);
+        __threadfence_system();  // the levels (and result) reach memory before ctl[1] says so
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            gnext = G + *(volatile int*)w.result;  // result[0] = D_k, written by this lane
+            __hip_atomic_store(a.ctl + 1, (unsigned)(k + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const long long gn = gnext;
+        G = (long long)(((unsigned long long)(unsigned)sgpr((int)(gn >> 32)) << 32) | (unsigned)sgpr((int)gn));
+    }
+}
+
 // ----------------------------------------------------------------------------------
 // host-side launchers (called from ga_host.cpp)
 int boundary_scratch_ints(int m, int n) { return (m + BSEG - 1) / BSEG + (n + BSEG - 1) / BSEG + 2; }
@@ -1989,6 +2085,13 @@ void launch_walk(hipStream_t s, const WalkArgs& w) {
     if (w.CB == 1) walk_kernel<1><<<1, 64 * WALK_WAVES, 0, s>>>(w);
     else if (w.CB == 2) walk_kernel<2><<<1, 64 * WALK_WAVES, 0, s>>>(w);
     else walk_kernel<4><<<1, 64 * WALK_WAVES, 0, s>>>(w);
+}
+
+void launch_walk_chain(hipStream_t s, const WalkChainArgs& a) {
+    const int CB = a.w[0].CB;
+    if (CB == 1) walk_chain_kernel<1><<<1, 64 * WALK_WAVES, 0, s>>>(a);
+    else if (CB == 2) walk_chain_kernel<2><<<1, 64 * WALK_WAVES, 0, s>>>(a);
+    else walk_chain_kernel<4><<<1, 64 * WALK_WAVES, 0, s>>>(a);
 }
 
 }  // namespace ga

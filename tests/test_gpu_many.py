@@ -107,3 +107,26 @@ def test_align_repeated_pipe_modes(monkeypatch, mode, fills, m, n, seed, count, 
         assert r.cost == cost
         assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == strings
     assert random.getstate()[1] == tuple(int(x) for x in ref[-1][2])
+
+
+@pytest.mark.parametrize("chain", ["1", "0"])
+@pytest.mark.parametrize("m,n,seed,count,kw", [
+    (700, 650, 13, 11, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+    (600, 640, 14, 9, dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)),
+    (40000, 300, 15, 7, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
+])
+def test_align_repeated_walk_chain(monkeypatch, chain, m, n, seed, count, kw):
+    """Walks chained in one launch (walk_chain_kernel, the default) and one launch per walk (GA_PIPE_CHAIN=0):
+    more alignments than slots (every slot reused), short walks that outrun the tie-break producer, a tall
+    pair; each alignment's strings and cost and the final random state equal the chained oracle's."""
+    import globalign_amd
+    monkeypatch.setenv("GA_PIPE_CHAIN", chain)
+    alpha = "protein" if "scoring_mat_name" in kw else "dna"
+    s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
+    ref = _chain_oracle(s1, s2, kw, seed, count)
+    random.seed(seed)
+    runs = globalign_amd.GlobalAligner(max_seq_len_prod=None, **kw).align_repeated(s1, s2, count)
+    for r, (cost, strings, _) in zip(runs, ref):
+        assert r.cost == cost
+        assert (r.seq_1_aligned, r.middle_part, r.seq_2_aligned) == strings
+    assert random.getstate()[1] == tuple(int(x) for x in ref[-1][2])
