@@ -1342,7 +1342,7 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
                 rc = fail(GA_E_TIMEOUT, "chained walk waited too long for its fill or tie-break entries");
                 break;
             }
-            std::this_thread::yield();
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
         if (rc != GA_OK) break;
         int res[16];

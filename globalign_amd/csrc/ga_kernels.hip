@@ -1928,7 +1928,8 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainAr
                     ok = 0;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                // ~3.4 us between polls: each is a PCIe read, and a walk may wait a whole fill (25 ms)
+                __builtin_amdgcn_s_sleep(127);
             }
             go = ok;
         }
