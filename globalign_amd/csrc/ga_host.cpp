@@ -1487,9 +1487,23 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     // experiment (GA_PIPE_ROW_FIRST=r): the first r fills through the row scan (shorter latency alone)
     int row_first = 0;
     if (const char* e = getenv("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
-    // fill j into slot j % S on fill stream j % F; each computes its own boundary
-    for (int k = 0; k < std::min(count, S); k++)
+    // fill j into slot j % S on fill stream j % F; each computes its own boundary.  Every fill of the
+    // pipeline computes the same arrays (the same pair, boundary and words), so walk k takes whichever
+    // pending slot's fill ended first, not slot k % S: in the ramp the third of four fills started at
+    // once ends ~3 ms after the fourth and ~3 ms after the third walk wanted it (GA_PIPE_SLOT_ORDER=fixed
+    // keeps slot k % S)
+    const bool any_order = [] {
+        const char* e = getenv("GA_PIPE_SLOT_ORDER");
+        return !(e && !strcmp(e, "fixed"));
+    }();
+    std::vector<int> pending;  // slots holding an enqueued fill no walk has taken, in enqueue order
+    std::vector<int> walk_slot((size_t)count, -1);
+    int fills_enqueued = 0;
+    for (int k = 0; k < std::min(count, S); k++) {
         if (int r = pipe_fill(c, k, fs[k % F], k < row_first)) return r;
+        pending.push_back(k);
+        fills_enqueued++;
+    }
     // the tie-break table: one continuous stream, extended by a host thread ahead of the walks (its
     // vectors are reserved up front: the walks read earlier entries while later ones are written)
     RngTable& R = c->many_rng;
@@ -1531,7 +1545,20 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     });
     // walk k over its table slice [G, G + per), after fill k, on the walk stream
     auto start_walk = [&](int k, int64_t G) -> int {
-        auto& sl = c->pipe[k % S];
+        // the slot: the first pending one whose fill has ended; while all are still running, the host
+        // waits for the first to end (the oldest is not always first: in the ramp four fills share the chip)
+        size_t pick = 0;
+        for (bool found = !any_order; !found;) {
+            for (size_t q = 0; q < pending.size() && !found; q++)
+                if (hipEventQuery(c->pipe[pending[q]].fdone) == hipSuccess) {
+                    pick = q;
+                    found = true;
+                }
+            if (!found) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        walk_slot[k] = pending[pick];
+        pending.erase(pending.begin() + (long)pick);
+        auto& sl = c->pipe[walk_slot[k]];
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return ready >= G + per; });
@@ -1548,7 +1575,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     int64_t Dmax = 0;
     float fill_sum = 0.f, walk_sum = 0.f;
     for (int k = 0; k < count && rc == GA_OK; k++) {
-        auto& sl = c->pipe[k % S];
+        auto& sl = c->pipe[walk_slot[k]];
         const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
                           ws, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
         auto step = [&]() -> int {
@@ -1581,16 +1608,19 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             }
             // alignment k's cost (fill k finished before walk k started) and walk time, before slot k's
             // pinned words and events are reused
-            const int* pin = c->pipe_pin + 8 * (k % S);
+            const int* pin = c->pipe_pin + 8 * walk_slot[k];
             if (pin[6]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
             cost_out[k] = (int64_t)pin[0] + pin[4] + pin[5];
             float f = 0.f;
             if (hipEventElapsedTime(&f, sl.f0, sl.f1) == hipSuccess) fill_sum += f;
             float wms = 0.f;
             if (hipEventElapsedTime(&wms, sl.w0, sl.w1) == hipSuccess) walk_sum += wms;
-            // fill k+S into slot k's buffers (walk k has read them), on its stream after fill k+S-F
-            if (k + S < count)
-                if (int r = pipe_fill(c, k % S, fs[(k + S) % F])) return r;
+            // the next fill into walk k's slot (walk k has read it), on its stream after the fill F before
+            if (fills_enqueued < count) {
+                if (int r = pipe_fill(c, walk_slot[k], fs[fills_enqueued % F])) return r;
+                pending.push_back(walk_slot[k]);
+                fills_enqueued++;
+            }
             // alignment k's strings, while walk k+1 and the fills run
             WalkStart st{m, n, 0, 0, 0, 1};
             int reason = 0;
