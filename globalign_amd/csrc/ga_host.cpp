@@ -1226,52 +1226,8 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
     HIPCHK(hipHostGetDevicePointer(&tab_dev, c->chain_tab, 0));
     HIPCHK(hipHostGetDevicePointer(&ctl_dev, ctl, 0));
 
-    // fill 0 first (it fixes the fill geometry and so the size of every slot's traceback words), then
-    // the walks' launch, so that its workgroup has a CU before the other fills take them all, then
-    // fills 1 .. S-1; fill j goes into slot j % S on fill stream j % F (each computes its own boundary)
-    int enqueued = 0, signalled = 0;
-    if (int r = pipe_fill(c, 0, fs[0])) return r;
-    enqueued++;
-    // every slot's fill buffers at their final size now: a reallocation's hipFree while the chain runs
-    // would wait for the chain, which waits for the host
-    const size_t tb_bytes = (size_t)c->nstripes * c->T * c->TC * 1024;
-    const size_t hand_bytes = sizeof(int2) * (size_t)c->nslabs * (m + 1);
-    for (int s = 1; s < S; s++) {
-        auto& sl = c->pipe[s];
-        HIPCHK(sl.tb.ensure(tb_bytes));
-        HIPCHK(sl.hand.ensure(hand_bytes));
-        HIPCHK(sl.flags.ensure(sizeof(unsigned) * 16));
-        HIPCHK(sl.out_last.ensure(sizeof(int) * 4));
-    }
-    ga::WalkChainArgs A{};
-    for (int s = 0; s < S; s++) {
-        auto& sl = c->pipe[s];
-        const WalkBufs wb{sl.tb.as<uint8_t>(), nullptr, sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          ws, nullptr, nullptr, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
-        A.w[s] = walk_args(c, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, wb);
-        A.w[s].result = reinterpret_cast<int*>(static_cast<uint8_t*>(io_dev) + io_stride * s);
-        A.w[s].ops = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(io_dev) + io_stride * s + 256);
-    }
-    A.tab = static_cast<const uint32_t*>(tab_dev);
-    A.ctl = static_cast<unsigned*>(ctl_dev);
-    A.tab_ready = reinterpret_cast<const long long*>(static_cast<unsigned*>(ctl_dev) + 4);
-    A.per = per;
-    A.wait_limit = 100ull * 1000 * 1000 * 60;  // 60 s of s_memrealtime (100 MHz)
-    A.count = count;
-    A.S = S;
-    HIPCHK(hipEventRecord(c->pipe[0].w0, ws));
-    ga::launch_walk_chain(ws, A);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->pipe[0].w1, ws));
-    for (int k = 1; k < std::min(count, S); k++) {
-        if (int r = pipe_fill(c, k, fs[k % F])) {
-            __atomic_store_n(ctl + 2, 1u, __ATOMIC_RELEASE);
-            (void)hipStreamSynchronize(ws);
-            return r;
-        }
-        enqueued++;
-    }
-    // the tie-break stream: a host thread extends it ahead of the walks, into pinned memory
+    // the tie-break stream: a host thread extends it ahead of the walks, into pinned memory; started
+    // before the fills are enqueued (C2 / C5: the first walk waited 2.1 / 4.0 ms for its entries)
     RngTable& R = c->many_rng;
     R.start(mt_state);
     R.tab.reserve((size_t)need);
@@ -1300,9 +1256,15 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
                 }
             }
             const double t1 = now_ms();
-            R.extend(want);
-            std::memcpy(c->chain_tab + from, R.tab.data() + from, sizeof(uint32_t) * (want - from));
-            __atomic_store_n(tab_ready, (long long)want, __ATOMIC_RELEASE);
+            // in pieces of half an alignment, each published as soon as it is written: the first walk
+            // waits for per entries, not for the three alignments' worth the producer starts with
+            for (int64_t to = from; to < want;) {
+                const int64_t nx = std::min(want, to + std::max<int64_t>(per / 2, 4096));
+                R.extend(nx);
+                std::memcpy(c->chain_tab + to, R.tab.data() + to, sizeof(uint32_t) * (nx - to));
+                __atomic_store_n(tab_ready, (long long)nx, __ATOMIC_RELEASE);
+                to = nx;
+            }
             rng_ms += now_ms() - t1;
             {
                 std::lock_guard<std::mutex> lk(mu);
@@ -1324,6 +1286,51 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
             for (int f = 0; f < F; f++) (void)hipStreamSynchronize(fs[f]);
         return rc;
     };
+    int enqueued = 0, signalled = 0;
+    auto launch_all = [&]() -> int {
+        // fill 0 first (it fixes the fill geometry and so the size of every slot's traceback words), then
+        // the walks' launch, so that its workgroup has a CU before the other fills take them all, then
+        // fills 1 .. S-1; fill j goes into slot j % S on fill stream j % F (each computes its own boundary)
+        if (int r = pipe_fill(c, 0, fs[0])) return r;
+        enqueued++;
+        // every slot's fill buffers at their final size now: a reallocation's hipFree while the chain runs
+        // would wait for the chain, which waits for the host
+        const size_t tb_bytes = (size_t)c->nstripes * c->T * c->TC * 1024;
+        const size_t hand_bytes = sizeof(int2) * (size_t)c->nslabs * (m + 1);
+        for (int s = 1; s < S; s++) {
+            auto& sl = c->pipe[s];
+            HIPCHK(sl.tb.ensure(tb_bytes));
+            HIPCHK(sl.hand.ensure(hand_bytes));
+            HIPCHK(sl.flags.ensure(sizeof(unsigned) * 16));
+            HIPCHK(sl.out_last.ensure(sizeof(int) * 4));
+        }
+        ga::WalkChainArgs A{};
+        for (int s = 0; s < S; s++) {
+            auto& sl = c->pipe[s];
+            const WalkBufs wb{sl.tb.as<uint8_t>(), nullptr, sl.ops.as<uint32_t>(), sl.result.as<int>(),
+                              ws, nullptr, nullptr, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+            A.w[s] = walk_args(c, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, wb);
+            A.w[s].result = reinterpret_cast<int*>(static_cast<uint8_t*>(io_dev) + io_stride * s);
+            A.w[s].ops = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(io_dev) + io_stride * s + 256);
+        }
+        A.tab = static_cast<const uint32_t*>(tab_dev);
+        A.ctl = static_cast<unsigned*>(ctl_dev);
+        A.tab_ready = reinterpret_cast<const long long*>(static_cast<unsigned*>(ctl_dev) + 4);
+        A.per = per;
+        A.wait_limit = 100ull * 1000 * 1000 * 60;  // 60 s of s_memrealtime (100 MHz)
+        A.count = count;
+        A.S = S;
+        HIPCHK(hipEventRecord(c->pipe[0].w0, ws));
+        ga::launch_walk_chain(ws, A);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(c->pipe[0].w1, ws));
+        for (int k = 1; k < std::min(count, S); k++) {
+            if (int r = pipe_fill(c, k, fs[k % F])) return r;
+            enqueued++;
+        }
+        return GA_OK;
+    };
+    if (int r = launch_all()) return stop(r);
     FILE* trace = nullptr;
     if (const char* tp = getenv("GA_PIPE_TRACE")) trace = fopen(tp, "a");
     const double h0 = now_ms();
@@ -1364,8 +1371,9 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
         walk_sum += res[8] / 1.0e5f;  // the walker's own time (s_memrealtime ticks, 100 MHz)
         if (trace)
             fprintf(trace, "{\"k\": %d, \"chain\": 1, \"fill_ms\": %.3f, \"walk_ms\": %.3f, \"walk_done_host\": %.3f, "
-                    "\"D\": %lld, \"tile_wait_us\": %.2f, \"tile_loads\": %d}\n", k, f, res[8] / 1.0e5,
-                    now_ms() - h0, (long long)Dk, res[6] / 100.0, res[11]);
+                    "\"D\": %lld, \"tile_wait_us\": %.2f, \"tile_loads\": %d, \"chain_wait_us\": %.2f, "
+                    "\"polls_fill\": %d, \"polls_tab\": %d}\n", k, f, res[8] / 1.0e5,
+                    now_ms() - h0, (long long)Dk, res[6] / 100.0, res[11], res[12] / 100.0, res[13], res[14]);
         // fill k+S into slot k's buffers (walk k has read them)
         if (k + S < count) {
             if (int r = pipe_fill(c, k % S, fs[(k + S) % F])) {

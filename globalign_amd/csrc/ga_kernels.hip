@@ -1915,14 +1915,19 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainAr
     __shared__ long long gnext;
     long long G = 0;
     for (int k = 0; k < a.count; k++) {
+        int wait_fill = 0, wait_tab = 0;  // polls that found the fill / the entries not ready (diagnostics)
+        unsigned long long t_wait = 0;
         if (threadIdx.x == 0) {
             int ok = 1;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 if (__hip_atomic_load(a.ctl + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) { ok = 0; break; }
-                if ((int)__hip_atomic_load(a.ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) > k &&
-                    __hip_atomic_load(const_cast<long long*>(a.tab_ready), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= G + a.per)
-                    break;
+                const bool fill_ok = (int)__hip_atomic_load(a.ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) > k;
+                const bool tab_ok = __hip_atomic_load(const_cast<long long*>(a.tab_ready), __ATOMIC_ACQUIRE,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM) >= G + a.per;
+                if (fill_ok && tab_ok) break;
+                wait_fill += !fill_ok;
+                wait_tab += !tab_ok;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.wait_limit) {
                     __hip_atomic_store(a.ctl + 3, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
                     ok = 0;
@@ -1932,12 +1937,18 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainAr
                 __builtin_amdgcn_s_sleep(127);
             }
             go = ok;
+            t_wait = __builtin_amdgcn_s_memrealtime() - t0;
         }
         __syncthreads();
         if (!sgpr(go)) return;  // uniform: the walks' control flow and arguments stay scalar
         __threadfence();  // acquire: the slot's traceback words and boundary, written by fill k
         const WalkArgs w = uniform_walk_args(a.w[k % a.S]);
         walk_body<CB>(w, a.tab + G);
+        if (threadIdx.x == 0) {  // result[12..14]: this walk's wait before it started (ticks, polls)
+            w.result[12] = (int)t_wait;
+            w.result[13] = wait_fill;
+            w.result[14] = wait_tab;
+        }
         __threadfence_system();  // the levels (and result) reach memory before ctl[1] says so
         __syncthreads();
         if (threadIdx.x == 0) {
