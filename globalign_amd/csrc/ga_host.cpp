@@ -1324,6 +1324,12 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
         ga::launch_walk_chain(ws, A);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->pipe[0].w1, ws));
+        if (const char* e = getenv("GA_CHAIN_STAGGER"); e && atoi(e) > 0) {
+            // experiment: fill 0 alone on the chip, the others after it (the first walk starts sooner)
+            HIPCHK(hipEventSynchronize(c->pipe[0].fdone));
+            signalled = 1;
+            __atomic_store_n(ctl, 1u, __ATOMIC_RELEASE);
+        }
         for (int k = 1; k < std::min(count, S); k++) {
             if (int r = pipe_fill(c, k, fs[k % F])) return r;
             enqueued++;
