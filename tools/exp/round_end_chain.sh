@@ -16,3 +16,4 @@ for f in ["bench_default", "bench_c5", "bench_c2"]:
     print(f, d["value"], round(d["ms_per_step"], 3), d["config"]["cost_matches_oracle"], d["config"].get("traceback_pin", {}).get("matches_oracle"))
 PY
 find gpurun_out/rc/prof_c5 -name "*stats*.csv" | sort
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()"
