@@ -1169,6 +1169,27 @@ int pipe_fill(ga_ctx* c, int slot, hipStream_t st, bool row = false) {
     return GA_OK;
 }
 
+// Per slot, pinned and coherent host memory for a pipelined walk's result words (256 B) and levels: the
+// walk writes them there, so the host reads them without a hipMemcpy (which would wait for a CU, and
+// the fills hold them all).  Returns the slot stride and the area's device address.
+int pipe_io(ga_ctx* c, int S, size_t* stride, uint8_t** dev) {
+    const size_t ops_bytes = (((size_t)(c->m + c->n + 1024) + 255) / 256) * 256, io_stride = 256 + ops_bytes;
+    if (c->chain_io_cap < io_stride * S) {
+        if (c->chain_io) HIPCHK(hipHostFree(c->chain_io));
+        c->chain_io = nullptr;
+        c->chain_io_cap = 0;
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, io_stride * S, hipHostMallocMapped | hipHostMallocCoherent));
+        c->chain_io = static_cast<uint8_t*>(hp);
+        c->chain_io_cap = io_stride * S;
+    }
+    void* d = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&d, c->chain_io, 0));
+    *stride = io_stride;
+    *dev = static_cast<uint8_t*>(d);
+    return GA_OK;
+}
+
 // align_many with its walks chained in one walk_chain_kernel launch.  Each walk used to
 // start after a host round trip (walk k's end seen by the host, its dispatch count read, walk k+1's
 // table slice copied and its kernel launched: 45-55 us at C2 / C5, 0.1-0.2 ms at C3), and by then a
@@ -1205,18 +1226,9 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
         HIPCHK(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
         c->chain_ctl = static_cast<unsigned*>(hp);
     }
-    const size_t ops_bytes = (((size_t)(m + n + 1024) + 255) / 256) * 256, io_stride = 256 + ops_bytes;
-    if (c->chain_io_cap < io_stride * S) {
-        if (c->chain_io) HIPCHK(hipHostFree(c->chain_io));
-        c->chain_io = nullptr;
-        c->chain_io_cap = 0;
-        void* hp = nullptr;
-        HIPCHK(hipHostMalloc(&hp, io_stride * S, hipHostMallocMapped | hipHostMallocCoherent));
-        c->chain_io = static_cast<uint8_t*>(hp);
-        c->chain_io_cap = io_stride * S;
-    }
-    void* io_dev = nullptr;
-    HIPCHK(hipHostGetDevicePointer(&io_dev, c->chain_io, 0));
+    size_t io_stride = 0;
+    uint8_t* io_dev = nullptr;
+    if (int r = pipe_io(c, S, &io_stride, &io_dev)) return r;
     auto res_host = [&](int s) { return reinterpret_cast<int*>(c->chain_io + io_stride * s); };
     auto ops_host = [&](int s) { return reinterpret_cast<uint32_t*>(c->chain_io + io_stride * s + 256); };
     unsigned* ctl = c->chain_ctl;
@@ -1510,6 +1522,22 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         const char* e = getenv("GA_PIPE_SLOT_ORDER");
         return !(e && !strcmp(e, "fixed"));
     }();
+    size_t io_stride = 0;
+    uint8_t* io_dev = nullptr;
+    if (int r = pipe_io(c, S, &io_stride, &io_dev)) return r;
+    // slot s's walk writes its result words and levels to pinned memory (pipe_io; GA_PIPE_PINNED_IO=0:
+    // to the slot's device buffers, read back with hipMemcpy)
+    const bool pinned_io = [] {
+        const char* e = getenv("GA_PIPE_PINNED_IO");
+        return !(e && atoi(e) == 0);
+    }();
+    auto walk_bufs = [&](int s) {
+        auto& sl = c->pipe[s];
+        return WalkBufs{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(),
+                        pinned_io ? reinterpret_cast<uint32_t*>(io_dev + io_stride * s + 256) : sl.ops.as<uint32_t>(),
+                        pinned_io ? reinterpret_cast<int*>(io_dev + io_stride * s) : sl.result.as<int>(), ws, sl.w0,
+                        sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+    };
     std::vector<int> pending;  // slots holding an enqueued fill no walk has taken, in enqueue order
     std::vector<int> walk_slot((size_t)count, -1);
     int fills_enqueued = 0;
@@ -1579,8 +1607,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         }
         HIPCHK(hipStreamWaitEvent(ws, sl.fdone, 0));
         std::memcpy(sl.tab_pin, tabp + G, sizeof(uint32_t) * per);
-        const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          ws, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+        const WalkBufs wb = walk_bufs(walk_slot[k]);
         return run_walk(c, sl.tab_pin, per, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, true, &wb);
     };
     int rc = start_walk(0, 0);
@@ -1590,13 +1617,15 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     float fill_sum = 0.f, walk_sum = 0.f;
     for (int k = 0; k < count && rc == GA_OK; k++) {
         auto& sl = c->pipe[walk_slot[k]];
-        const WalkBufs wb{sl.tb.as<uint8_t>(), sl.rng.as<uint32_t>(), sl.ops.as<uint32_t>(), sl.result.as<int>(),
-                          ws, sl.w0, sl.w1, sl.bnd_row.as<int>(), sl.bnd_col.as<int>()};
+        const WalkBufs wb = walk_bufs(walk_slot[k]);
+        const int* res_pin = reinterpret_cast<const int*>(c->chain_io + io_stride * walk_slot[k]);
+        const uint32_t* ops_pin = reinterpret_cast<const uint32_t*>(c->chain_io + io_stride * walk_slot[k] + 256);
         auto step = [&]() -> int {
             // walk k done: its dispatch count fixes where walk k+1's table slice starts
             HIPCHK(hipEventSynchronize(sl.w1));
             int res[16];
-            HIPCHK(hipMemcpy(res, sl.result.p, sizeof(int) * 16, hipMemcpyDeviceToHost));
+            if (pinned_io) std::memcpy(res, res_pin, sizeof(res));
+            else HIPCHK(hipMemcpy(res, sl.result.p, sizeof(int) * 16, hipMemcpyDeviceToHost));
             const int64_t Dk = res[0];
             Dmax = std::max(Dmax, Dk);
             if (trace) {
@@ -1642,7 +1671,9 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             char* a_k = oa + (size_t)k * cap;
             char* m_k = om + (size_t)k * cap;
             char* b_k = ob + (size_t)k * cap;
-            if (int r = decode_segment(c, res, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, wb, true)) return r;
+            if (int r = decode_segment(c, res, st, reason, a_chr, b_chr, a_k, m_k, b_k, cap, len, wb, true,
+                                       pinned_io ? ops_pin : nullptr))
+                return r;
             if (int r = conclude_walk(R, st, reason, nullptr, a_chr, b_chr, a_k, m_k, b_k, cap, len, &out_len[k],
                                       &tb_status[k]))
                 return r;
