@@ -35,7 +35,7 @@ import time
 # The repeated-alignment pipeline runs four fill streams beside the walk stream, all at the greatest
 # priority, whose pool holds GPU_MAX_HW_QUEUES hardware queues per process (HIP's default 4; two streams on
 # one in-order queue serialise).  Set before anything initialises the HIP runtime.
-os.environ["GPU_MAX_HW_QUEUES"] = "8"
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # a caller's own setting is kept
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -358,6 +358,7 @@ struct ga_ctx {
     int walk_cus = -1;  // CUs reserved for the walk (0: no masks; -1: not yet set up)
     int* pipe_pin = nullptr;       // pinned: per slot {out_last[4], GV(m), GH(n), abort, pad}
     int pipe_fills = 2, pipe_slots = 3;  // fills in flight (one stream each) and slots (fills + the walked one)
+    int hw_queues = 4;                   // GPU_MAX_HW_QUEUES as the process first saw it (ga_ctx_create)
     int pipe_lane_td = 0, pipe_lane_nwc = 0;  // the pipeline's lane-kernel fill geometry (0: the row scan)
     RngTable many_rng;
     // chained pipeline walks (walk_chain_kernel): the tie-break stream in pinned, coherent host memory
@@ -1455,8 +1456,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // and the walk stream share a priority's pool of GPU_MAX_HW_QUEUES queues; two streams on one
         // in-order queue serialise): C3 steady state 8.34 -> 7.81 ms per alignment, walk-bound
         // (tools/exp/pipe_queues.sh); three with HIP's default of four queues
-        const char* hq = getenv("GPU_MAX_HW_QUEUES");
-        const int queues = hq ? atoi(hq) : 4;
+        const int queues = c->hw_queues;
         // row-scan fills: three in flight (four streams with the walk's: HIP's default pool holds them);
         // with the faster walk C5 is no longer walk-bound (1.80 -> 1.51 ms per alignment), C2 unchanged
         int F = lane ? (queues >= 5 ? 4 : 3) : 3;
@@ -1726,6 +1726,16 @@ int ga_ctx_create(int device, ga_ctx** out) {
     HIPCHK(hipSetDevice(device));
     ga_ctx* c = new ga_ctx();
     c->device = device;
+    {
+        // hardware queues per priority pool: what the HIP runtime read when it started, i.e. the variable
+        // as the process first saw it here (a later change, e.g. a module setting it after HIP started,
+        // does not change the runtime's queues)
+        static const int hwq = [] {
+            const char* e = getenv("GPU_MAX_HW_QUEUES");
+            return e && atoi(e) > 0 ? atoi(e) : 4;
+        }();
+        c->hw_queues = hwq;
+    }
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)

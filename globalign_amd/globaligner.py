@@ -84,6 +84,8 @@ class GlobalAligner:
         good = validate_and_transform_args(None, None, seq_1, seq_2, max_seq_len_prod=self.max_seq_len_prod,
                                            **self.settings)
         s1, s2, scoring_mat, costing_mat, gos, goc, output = good
+        if int(count) <= 0:
+            return []  # a loop of zero find_global_alignment calls
         if len(self.devices) > 1 or not self.traceback or min(len(s1), len(s2)) < 2:
             # (degenerate lengths may raise the reference's IndexError mid-way: one call at a time)
             return [_align_validated(good, device=self.device, traceback=self.traceback, devices=self.devices)
@@ -91,12 +93,16 @@ class GlobalAligner:
         tables = _native.CostTables(costing_mat, goc)
         eng = _native.default_engine(self.device)
         eng.load(tables.codes(s1), tables.codes(s2), tables)
-        runs, mt = eng.align_many(_mt_words(), s1, s2, int(count))
+        mt0 = _mt_words()
+        runs, mt = eng.align_many(mt0, s1, s2, int(count))
+        if any(status == _native.GA_TB_INDEX_ERROR for _, _, status in runs):
+            # consecutive reference calls stop at the first IndexError, with the random state that call
+            # left: replay them one at a time from the starting state (never reached for min(m, n) >= 2)
+            _set_mt_words(mt0)
+            return [_align_validated(good, device=self.device, traceback=True) for _ in range(int(count))]
         _set_mt_words(mt)
         out = []
         for cost, (a, mid, b), status in runs:
-            if status == _native.GA_TB_INDEX_ERROR:
-                raise IndexError("string index out of range")
             score = final_cost_to_score(cost=cost, m=len(s1), n=len(s2), max_score=get_max_val(scoring_mat))
             out.append(AlignmentResults(a, mid, b, cost, score, scoring_mat, costing_mat, gos, goc, output))
         return out

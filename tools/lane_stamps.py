@@ -42,6 +42,9 @@ tot = np.maximum(st[:, 5], 1)
 simd = (st[:, 6] >> 4) & 3
 wave_in_wg = np.arange(ns) % nwc
 lag = np.diff(start)
+# every stripe runs the same rows at the same busy pace once its left edge arrives, so consecutive
+# stripes' END times differ by the hand-over lag between them (the start stamps are the kernel's start)
+elag = np.diff(end)
 cross = np.array([(k + 1) % nwc == 0 for k in range(ns - 1)], dtype=bool)
 by_simd = {}
 for sd in range(4):
@@ -61,6 +64,10 @@ print(json.dumps({
     "last_end_us": float(end.max()), "last_start_us": float(start.max()),
     "lag_intra_wg_us": float(np.mean(lag[~cross])) if (~cross).any() else None,
     "lag_cross_wg_us": float(np.mean(lag[cross])) if cross.any() else None,
+    "end_lag_intra_wg_us": float(np.median(elag[~cross])) if (~cross).any() else None,
+    "end_lag_cross_wg_us": float(np.median(elag[cross])) if cross.any() else None,
+    "end_lag_mean_us": float(np.mean(elag)) if len(elag) else None,
+    "end_lag_by_wave_us": {int(w): float(np.median(elag[(np.arange(ns - 1) % nwc) == w])) for w in range(min(nwc, ns - 1))},
     "stripe_dur_us_median": float(np.median(dur)), "stripe_dur_us_max": float(dur.max()),
     "ns_per_step_median": float(np.median(dur) * 1e3 / (m + 63)),
     "cycles_per_step_median": float(np.median(tot / (m + 63))),
