@@ -217,13 +217,14 @@ class Engine:
         return cost.value, out
 
     def fill_kind(self):
-        """The kernel and geometry of the last fill: (kind, T, nstripes, nwc, nslabs), kind 'row' / 'diag' / 'lane'."""
+        """The kernel and geometry of the last fill: (kind, T, nstripes, nwc, nslabs), kind 'row' / 'diag' / 'lane', or
+        'rc' (the recompute walk's checkpointing lane fill)."""
         f = self._L.ga_debug_fill_kind
         f.argtypes = [C.c_void_p, C.c_void_p]
         f.restype = C.c_int
         out = np.zeros(5, dtype=np.int32)
         _check(f(self._h, out.ctypes.data))
-        return (("row", "diag", "lane")[int(out[0])],) + tuple(int(x) for x in out[1:])
+        return (("row", "diag", "lane", "rc")[int(out[0])],) + tuple(int(x) for x in out[1:])
 
     def set_cells(self, cells):
         """Use a filled (m+1, n+1, 3) int32 cell array for the next traceback (-> min of the last cell)."""

@@ -42,6 +42,11 @@ struct FillArgs {
     unsigned long long* dbg;  // optional timestamps: [nstripes][8] or nullptr
     int2* ckpt;               // banded traceback: (H', h2') of rows ckpt_rows, 2*ckpt_rows, ... (< m) or nullptr
     int ckpt_rows;            //   [row / ckpt_rows - 1][n + 1]; a multiple of FROWS
+    // recompute checkpoints of the lane fill (nullptr: none)
+    int2* colck;              // [nstripes][m + 1]: (H', h1') of every stripe's right edge column, rows 1..m
+    int2* stck;               // staircase lane states after step k*stck_every - 1, k = 1 .. (m - 1) / stck_every:
+                              //   [k - 1][nstripes][TD + 1][64]: (H'[c], h2'[c]) for c < TD, then (h1' carry, H' diag)
+    int stck_every;           //   a multiple of 32 (a pair of 16-step sub-chunks)
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),
@@ -67,6 +72,40 @@ struct WalkArgs {
     unsigned* dbg;        // optional: per tile need (ti, tj, D, wait ticks) x WALK_DBG entries, or nullptr
     int skip_corners;     // loaders leave the block's far off-diagonal tiles (offsets (3,0), (0,3), (3,1), (1,3))
     int nloaders;         // loader waves: 12, 13 (+ the idle wave 12) or 14 (+ wave 8, no L2 prefetcher)
+    // the recompute walk (walk_rc_kernel; unused by the other walks)
+    const unsigned* rc_flags;  // [nbi][nbs] per 64-row block of a fill stripe: rc_ready once its words are written
+    unsigned rc_ready;
+    int rc_nbs, rc_td;         // blocks per block row; 64-column tiles per block (the fill's TD)
+    unsigned* rc_pos;          // [0] the walker's tile (ti << 16 | tj), [1] 1 once the walk has ended
+};
+
+// The recompute walk's tile cache: block (bi, bs) (64 rows of fill stripe bs) lives at slot
+// (bi mod RC_CACHE, bs mod RC_CACHE); the recompute window (8 x 8 blocks up-left of the walker) never
+// reaches a slot the walker may still read
+constexpr int RC_CACHE = 16;
+
+// The recompute workgroups of walk_rc_kernel (ga_rcwalk.hip): each wave recomputes 64-row
+// blocks of one fill stripe (64*TD columns) from the lane fill's checkpoints, writing their traceback words.
+struct RcArgs {
+    const uint8_t* a;      // m codes
+    const uint8_t* b;      // n codes (this slab's columns)
+    const int* subp;       // K x K sub'
+    int K;
+    const int2* top;       // [n+1] (H', h2') of row 0
+    const int2* left;      // [m+1] (H', h1') of column 0
+    const int2* colck;     // [nstripes][m+1] right edges (FillArgs::colck)
+    const int2* stck;      // staircase states (FillArgs::stck)
+    int stck_every;
+    uint8_t* tb;           // traceback words (ga_device.h layout), TC 16-byte words per lane per 64-column stripe
+    int TC, m, n, o;
+    int TD, nstripes, nbi, nbs;  // nbs = nstripes; nbi = 64-row blocks
+    unsigned* flags;       // [nbi][nbs]: < 2*epoch free, 2*epoch claimed, 2*epoch + 1 ready
+    unsigned epoch;
+    unsigned* pos;         // the walk's WalkArgs::rc_pos
+    int workers;           // waves per workgroup that recompute (the rest leave)
+    int worker_bytes;      // LDS per worker
+    unsigned spin_limit;   // idle polls before a worker gives up (the walk then reports its own timeout)
+    unsigned char off[64]; // window offsets (dbi << 4 | dbs) from the walker's block, nearest first
 };
 
 // Pipelined walks in one launch (walk_chain_kernel): walk k uses w[k % S] with rng = tab + G_k.
@@ -89,6 +128,9 @@ void launch_fill(hipStream_t s, const FillArgs& p, int CB, int qbytes, bool tb, 
 size_t fill_lds_bytes(int nwc, int qbytes, int K, int qrows, int tb_stage_bytes_per_wave = 0);
 void launch_walk(hipStream_t s, const WalkArgs& w);
 void launch_walk_chain(hipStream_t s, const WalkChainArgs& a);
+// the recompute walk: one walker workgroup + nserv recompute workgroups (ga_rcwalk.hip)
+void launch_walk_rc(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv);
+int rc_worker_bytes(int TD, int CB, int stck_every);
 // traceback words of a caller-supplied (m+1) x (n+1) x 3 cell array (dp_array_backward shim)
 void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)

@@ -379,6 +379,11 @@ struct ga_ctx {
     bool dbg_on = false;
     int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
     DevBuf dbg, wdbg;
+    // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
+    DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
+    unsigned rc_epoch = 0;
+    bool rc_used = false;  // the last ga_problem_align took the recompute path
+    int rc_T = 0;          // its fill stripe width (64-column tiles per block)
 };
 
 namespace {
@@ -595,6 +600,10 @@ struct Band {
     int64_t nc = 0;             // columns 1..nc only (0: all): the walk enters the band at column nc
     const int2* top = nullptr;  // (H', h2') of row r0, [n+1] (column 0 = the left edge's corner)
     bool band = false;          // fill rows r0+1 .. r0+mb only (the boundary is already computed)
+    // the recompute walk's score fill: the lane kernel with its checkpoints (every stripe's
+    // right edge, the staircase lane states every rc_every steps) into ctx->colck / ctx->stck
+    bool rc = false;
+    int rc_every = 64;
     int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
     int ckpt_rows = 0;
     // pipelined alignments (align_many): a fill with buffers and a stream of its own, so that two
@@ -631,7 +640,12 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // score only: the lane-skewed kernel when its chain's skew (~74 steps per stripe)
     // is short against the m rows every stripe walks (measured: 1M x 125k 60 ms against 107 for the row
     // scan, C4 244 against 312; 100k x 100k, whose 782 stripes add 58k steps of skew, 13.5 against 12.6)
-    if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
+    if (bd.rc) {
+        if (tb || full || !lane_geometry(c, n, &qrows, false)) return fail(GA_E_STATE, "recompute fill needs the lane kernel");
+        // the checkpointing variant runs 16-step sub-chunks (8 waves at TD = 8 would take 8-step ones)
+        if (c->nwc == 8 && c->T == 8 && !lane_geometry(c, n, &qrows, false, 8, 4)) return fail(GA_E_STATE, "recompute fill geometry");
+        c->lane = true;
+    } else if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
         c->lane = lane_geometry(c, n, &qrows, tb, bd.lane_td, bd.lane_nwc, 2048);
     else if (!full && (bd.ckpt == nullptr || !tb) && (c->diag_req == 3 || (c->diag_req == 0 && !tb)) &&
              lane_geometry(c, n, &qrows, tb) && (c->diag_req == 3 || 4 * 74 * (int64_t)c->nstripes <= m))
@@ -700,6 +714,16 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.a = c->a.as<uint8_t>() + bd.r0;
     p.ckpt = bd.ckpt;
     p.ckpt_rows = bd.ckpt_rows;
+    p.colck = nullptr;
+    p.stck = nullptr;
+    p.stck_every = bd.rc_every;
+    if (bd.rc) {
+        const int64_t nck = std::max<int64_t>((m - 1) / bd.rc_every, 1);
+        HIPCHK(c->colck.ensure(sizeof(int2) * (size_t)c->nstripes * (m + 1)));
+        HIPCHK(c->stck.ensure(sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64));
+        p.colck = c->colck.as<int2>();
+        p.stck = c->stck.as<int2>();
+    }
     p.subp = c->qp.as<int>();
     p.K = c->K;
     p.b = c->b.as<uint8_t>() + c->col0;
@@ -1063,6 +1087,124 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
     }
     c->walk_ms = walk_ms;
     c->fill_ms = fill_ms;
+    const int rc = conclude_walk(R, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
+    c->call_ms = (float)(now_ms() - t0);
+    return rc;
+}
+
+// ---------------------------------------------------------------- the recompute walk
+// One find_global_alignment without stored traceback words: a score-only lane fill that leaves
+// checkpoints, then one launch in which a workgroup walks while recompute workgroups write the
+// traceback words of the 64-row blocks ahead of it into a small tile cache.  The fill runs at score-only
+// speed and memory is O(checkpoints), not m*n words.
+bool rc_eligible(ga_ctx* c) {
+    const char* e = getenv("GA_RC");  // 0: never; 1: whenever the shape allows (tests); default: large problems
+    const int mode = e ? atoi(e) : -1;
+    if (mode == 0 || c->slab || c->qbytes != 1 || c->K > 32) return false;
+    if (c->m < 256 || c->n < 256) return false;  // (degenerate walks read cells no block ever recomputes)
+    if (mode == 1) return true;
+    int64_t min_cells = (int64_t)1 << 27;
+    if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
+    return c->m * c->n >= min_cells;
+}
+
+int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
+             int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const double t0 = now_ms();
+    const int64_t m = c->m, n = c->n;
+    Band bd;
+    bd.rc = true;
+    // checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps;
+    // wider spacing trades recompute steps for checkpoint memory (TD + 1) * 512 B per stripe per spacing
+    bd.rc_every = 64;
+    if (const char* e = getenv("GA_RC_EVERY")) bd.rc_every = std::max(64, (atoi(e) / 32) * 32);
+    {
+        // memory: halve the spacing's checkpoint bytes until they fit a budget (default 96 GB)
+        int64_t budget = (int64_t)96 << 30;
+        if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
+        const int64_t stripes = (n + 63) / 64;  // an upper bound at any TD: (TD + 1) / TD <= 2 per 64 columns
+        while ((m / bd.rc_every) * stripes * 2 * 512 > budget && bd.rc_every < 4096) bd.rc_every *= 2;
+    }
+    c->rc_used = true;
+    if (int r = enqueue_fill(c, 0, bd)) return r;
+    const int TD = c->T;
+    c->rc_T = TD;
+    const int CB = c->CB;
+    const int nbi = (int)((m + 63) / 64), nbs = c->nstripes;
+    HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE * ga::RC_CACHE * TD * 64 * 64 * CB));
+    const size_t nflags = (size_t)nbi * nbs;
+    if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_epoch >= 0x7ffffff0u) {
+        HIPCHK(c->rc_flags.ensure(nflags * sizeof(unsigned)));
+        HIPCHK(hipMemsetAsync(c->rc_flags.p, 0, c->rc_flags.cap, c->stream));
+        c->rc_epoch = 0;
+    }
+    c->rc_epoch++;
+    HIPCHK(c->rc_pos.ensure(16));
+    HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, c->stream));
+    // the tie-break table on the host while the device fills
+    RngTable R;
+    const double t1 = now_ms();
+    build_rng(mt_state, m + n + 1, R);
+    c->rng_ms = (float)(now_ms() - t1);
+    WalkBufs wb = ctx_walk_bufs(c);
+    wb.tb = c->rc_tb.as<uint8_t>();
+    const int64_t ntab = (int64_t)R.tab.size();
+    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    ga::WalkArgs w = walk_args(c, ntab, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, wb);
+    w.TC = ga::RC_CACHE * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
+    w.nloaders = 14;                  // no L2 prefetcher (it would read blocks not yet recomputed)
+    w.rc_flags = c->rc_flags.as<unsigned>();
+    w.rc_ready = 2u * c->rc_epoch + 1u;
+    w.rc_nbs = nbs;
+    w.rc_td = TD;
+    w.rc_pos = c->rc_pos.as<unsigned>();
+    ga::RcArgs r{};
+    r.a = c->a.as<uint8_t>();
+    r.b = c->b.as<uint8_t>() + c->col0;
+    r.subp = c->qp.as<int>();
+    r.K = c->K;
+    r.top = c->top.as<int2>() + c->col0;
+    r.left = c->left.as<int2>();
+    r.colck = c->colck.as<int2>();
+    r.stck = c->stck.as<int2>();
+    r.stck_every = bd.rc_every;
+    r.tb = c->rc_tb.as<uint8_t>();
+    r.TC = w.TC;
+    r.m = (int)m;
+    r.n = (int)n;
+    r.o = c->o;
+    r.TD = TD;
+    r.nstripes = c->nstripes;
+    r.nbi = nbi;
+    r.nbs = nbs;
+    r.flags = c->rc_flags.as<unsigned>();
+    r.epoch = c->rc_epoch;
+    r.pos = c->rc_pos.as<unsigned>();
+    r.worker_bytes = ga::rc_worker_bytes(TD, CB, bd.rc_every);
+    r.workers = std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
+    r.spin_limit = 1u << 20;
+    {
+        // the window: 8 x 8 blocks up-left of the walker's, nearest first (tile distance dbi + dbs * TD)
+        std::vector<std::pair<int, int>> off;
+        for (int di = 0; di < 8; di++)
+            for (int dj = 0; dj < 8; dj++) off.push_back({di * 16 + dj, di + dj * TD});
+        std::stable_sort(off.begin(), off.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+            return x.second < y.second;
+        });
+        for (int k = 0; k < 64; k++) r.off[k] = (unsigned char)off[k].first;
+    }
+    int nserv = 24;
+    if (const char* e = getenv("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
+    HIPCHK(hipEventRecord(wb.ev0, wb.stream));
+    ga::launch_walk_rc(wb.stream, w, r, nserv);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(wb.ev1, wb.stream));
+    if (int rr = finish_fill(c, cost_out, nullptr)) return rr;
+    WalkStart st{m, n, 0, 0, 0, 1};
+    int reason = 0;
+    int64_t len = 0;
+    if (int rr = walk_segment(c, st, reason, a_chr, b_chr, oa, om, ob, cap, len, &wb)) return rr;
+    if (reason == 7) return fail(GA_E_TIMEOUT, "recompute walk: a tile was never recomputed");
     const int rc = conclude_walk(R, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
     return rc;
@@ -1822,6 +1964,7 @@ int ga_problem_set(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b, int
 }
 
 int ga_problem_fill(ga_ctx* c, int32_t flags, int64_t* cost_out, int32_t* full_out) {
+    if (c) c->rc_used = false;
     if (int r = check_ctx(c)) return r;
     if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
     if ((flags & GA_FILL_FULL) && !full_out) return fail(GA_E_ARG, "GA_FILL_FULL needs full_out");
@@ -1865,6 +2008,8 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     if (int r = check_ctx(c)) return r;
     if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
+    c->rc_used = false;
+    if (rc_eligible(c)) return rc_align(c, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
     if (const int64_t Bh = band_rows(c)) return banded_align(c, Bh, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len,
                                                              tb_status, cost_out);
     const double t0 = now_ms();
@@ -2077,7 +2222,7 @@ int ga_debug_geometry(ga_ctx* c, int32_t* out4) {
 // and its geometry {T, nstripes, nwc, nslabs}.
 int ga_debug_fill_kind(ga_ctx* c, int32_t* out5) {
     if (!c || !out5) return fail(GA_E_ARG, "null argument");
-    out5[0] = c->lane ? 2 : c->diag ? 1 : 0;
+    out5[0] = c->rc_used ? 3 : c->lane ? 2 : c->diag ? 1 : 0;  // 3: the recompute walk's lane fill
     out5[1] = c->T;
     out5[2] = c->nstripes;
     out5[3] = c->nwc;

@@ -44,7 +44,12 @@ size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
 // sub-chunk (8 or 16: the edge / profile reads, the publish and the waits are paid once per SUB steps)
 // CKP: the banded traceback's score pass, storing the checkpoint rows (a variant of its own: the extra
 // paths cost the plain score fill registers)
-template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false>
+// RC: the recompute checkpoints (score only): every stripe's right edge to p.colck (lanes
+// 64-SUB..63's shift registers after each sub-chunk, 128 B per store) and, every p.stck_every steps, each
+// lane's whole state (its columns' H' and h2', the h1' it hands right, the diagonal H' it took from the
+// left) to p.stck: a staircase (lane l at row k*stck_every - l) from which any 64-row tile of the stripe
+// is recomputed with the same steps (ga_rcwalk.hip)
+template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false, bool RC = false>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -385,6 +390,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             : "=&s"(saved)
             : "v"(oaddr), "v"(hx), "v"(pcl), "s"(om), "v"(cp)
             : "memory");
+        if constexpr (RC) {
+            // lane 64-SUB+u holds row rlo+u of this stripe's right edge
+            const int row = rlo + lane - (64 - SUB);
+            if (lane >= 64 - SUB && row >= 1 && row <= m) p.colck[(long long)s * (m + 1) + row] = make_int2(RH, RX);
+        }
     };
     // traceback words: window w of 16 steps done -> aligned word w - 1 - lane/16 of every column (LkRot)
     auto emit = [&](int win) {
@@ -426,6 +436,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
             emit(it);
         }
+        if constexpr (RC) {
+            // staircase checkpoint k after step k*E - 1: lane 0 has finished row k*E, lane l row k*E - l
+            const int done = r0 + 2 * SUB;
+            if (done % p.stck_every == 0 && done < m) {
+                int2* ck = p.stck + ((long long)(done / p.stck_every - 1) * p.nstripes + s) * (TD + 1) * 64 + lane;
+#pragma unroll
+                for (int k = 0; k < TD; k++) ck[k * 64] = make_int2(H[k], Y[k]);
+                ck[TD * 64] = make_int2(Xl, HLp);
+            }
+        }
     }
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
@@ -454,6 +474,14 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     }();
     const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
+    if constexpr (CB == 0 && !DBG && SUB == 16) {
+        if (p.stck != nullptr) {
+            auto* fc = fill_lane_kernel<NWC, TD, 0, 16, false, false, true>;
+            (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            return;
+        }
+    }
     if constexpr (CB == 0 && !DBG) {
         if (p.ckpt != nullptr) {  // 8-step sub-chunks: with 16 the checkpoint stores spill at TD >= 4
             auto* fc = fill_lane_kernel<NWC, TD, CB, 8, false, true>;

@@ -1,0 +1,238 @@
+// ga_rcwalk.hip -- the recompute walk (dp_array_backward, globaligner.py:395-593).
+//
+// The whole-problem fill stores no traceback words: the lane fill (ga_lane.hip, RC variant) leaves only
+// checkpoints -- every stripe's right edge column and, every stck_every steps, each lane's state (a
+// staircase across the stripe).  One launch then runs the walk and the traceback words it needs side by
+// side:
+//   workgroup 0   the walk (walk_body, ga_walk.h) with its loaders reading 64x64 tiles of words from a
+//                 small direct-mapped cache in HBM, each tile once its block's flag says it is written;
+//   workgroups 1+ recompute workers, one per wave: a worker claims (CAS on the block's flag) the nearest
+//                 block of the window ahead of the walker that nobody has claimed, re-runs the lane fill's
+//                 steps for it from the staircase checkpoint above (up to stck_every + 126 steps of the
+//                 stripe's 64*TD columns), stages the cells' traceback codes in LDS and writes the block's
+//                 words into the cache with write-through (sc1) stores, then the flag.
+// A block is 64 rows of one fill stripe: TD walker tiles.  The walk path only moves up and left, so the
+// window (8 x 8 blocks up-left of the walker's block) always holds the tiles it can reach next, and a
+// 16 x 16-block cache never overwrites a block the walker may still read.  The words are the ones the
+// full traceback fill writes (lk_code of the same exact int32 cells), so the walk is unchanged.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ga_device.h"
+#include "ga_lane.h"
+#include "ga_sync.h"
+#include "ga_walk.h"
+
+namespace ga {
+
+constexpr int RC_ROWS = 64;   // rows per block (one walker tile row)
+
+__host__ __device__ inline int rc_sp(int CB) { return 64 * CB + 16; }      // stage bytes per column (+16: banks)
+__host__ __device__ inline int rc_aw(int every) { return every + 256; }    // a-window dwords / edge-window rows
+int rc_worker_bytes(int TD, int CB, int every) {
+    return 64 * TD * rc_sp(CB) + 16 + rc_aw(every) * 4 + rc_aw(every) * 8;
+}
+
+__device__ __forceinline__ void st16_sc1(uint4* p, uint4 v) {
+    const wk_u4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+
+// Recompute block (bi, bs): rows 64*bi+1 .. 64*bi+64 of fill stripe bs, its traceback words into the cache.
+template <int TD, int CB>
+__device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int bi, int bs, int lane) {
+    const int SP = rc_sp(CB), AW = rc_aw(r.stck_every);
+    uint8_t* stage = wl;                                                  // [64*TD columns][SP]
+    uint32_t* awin = reinterpret_cast<uint32_t*>(wl + 64 * TD * SP + 16);  // dword i: a[base+i .. base+i+3]
+    int2* ewin = reinterpret_cast<int2*>(awin + AW);                      // left edge of rows t0+1 ..
+    const int m = r.m, n = r.n, o = r.o;
+    const int R0 = bi * RC_ROWS;
+    const int nrow = min(RC_ROWS, m - R0);
+    const int ck = R0 / r.stck_every;  // the staircase checkpoint above the block (0: row 0)
+    const int t0 = ck * r.stck_every;
+    const int nst = ((R0 + nrow + 62) - t0 + 1 + 3) & ~3;  // steps, whole groups of 4 (lane 63 ends the block)
+    const int base = t0 - 63;                               // a index of lane 63's row at step t0
+    const int s = bs;
+    const int j0 = s * 64 * TD, jl = j0 + lane * TD;
+    for (int i = lane; i < nst + 64; i += 64) {  // (a lane reads dwords up to nst + 59)
+        uint32_t v = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int x = base + i + u;
+            v |= (x >= 0 && x < m) ? (uint32_t)r.a[x] << (8 * u) : 0u;
+        }
+        awin[i] = v;
+    }
+    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
+    for (int i = lane; i < nst; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
+    int bcode[TD];
+    int H[TD], Y[TD];
+    int Xl = 0, HLp = 0;
+#pragma unroll
+    for (int c = 0; c < TD; c++) bcode[c] = jl + c + 1 <= n ? r.b[jl + c] : 0;
+    if (ck == 0) {
+#pragma unroll
+        for (int c = 0; c < TD; c++) {
+            const int2 t = r.top[min(jl + c + 1, n)];
+            H[c] = t.x;
+            Y[c] = t.y;
+        }
+        HLp = r.top[min(jl, n)].x;
+    } else {
+        const int2* st = r.stck + ((long long)(ck - 1) * r.nstripes + s) * (TD + 1) * 64 + lane;
+#pragma unroll
+        for (int c = 0; c < TD; c++) {
+            const int2 v = st[c * 64];
+            H[c] = v.x;
+            Y[c] = v.y;
+        }
+        const int2 v = st[TD * 64];
+        Xl = v.x;
+        HLp = v.y;
+    }
+    int Hl = H[TD - 1];
+    const unsigned op1 = (unsigned)o + 1u;
+    uint8_t* dummy = stage + 64 * TD * SP;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the windows written by this wave
+    __builtin_amdgcn_wave_barrier();
+    for (int g = 0; g < nst; g += 4) {
+        const int t = t0 + g;
+        const uint32_t aw = awin[t - lane - base];  // this lane's a codes at steps t .. t+3
+        int sb[4][TD];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int ac = (int)((aw >> (8 * u)) & 0xffu) * 32;
+#pragma unroll
+            for (int c = 0; c < TD; c++) sb[u][c] = stab[ac + bcode[c]];
+        }
+        const int4 e01 = *reinterpret_cast<const int4*>(ewin + g);
+        const int4 e23 = *reinterpret_cast<const int4*>(ewin + g + 2);
+        const int eh[4] = {e01.x, e01.z, e23.x, e23.z}, ex[4] = {e01.y, e01.w, e23.y, e23.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int row = t + u - lane + 1;
+            const bool act = row >= 1;
+            const bool inr = row > R0 && row <= R0 + nrow;
+            int X = __builtin_amdgcn_update_dpp(ex[u], Xl, 0x138, 0xf, 0xf, false);   // h1'(row, left)
+            const int HLn = __builtin_amdgcn_update_dpp(eh[u], Hl, 0x138, 0xf, 0xf, false);
+            int Hd = HLp;
+#pragma unroll
+            for (int c = 0; c < TD; c++) {
+                const int M = Hd + sb[u][c];
+                const int Hn = min(min(M, X), Y[c]);
+                const unsigned code = lk_code<CB>(M, X, Y[c], Hn, op1);
+                uint8_t* dst = inr ? stage + (lane * TD + c) * SP + (row - R0 - 1) * CB : dummy;
+                if constexpr (CB == 1) *dst = (uint8_t)code;
+                else if constexpr (CB == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)code;
+                else *reinterpret_cast<uint32_t*>(dst) = code;
+                const int Ho = Hn + o;
+                X = min(X, Ho);
+                Y[c] = act ? min(Y[c], Ho) : Y[c];
+                Hd = H[c];
+                H[c] = act ? Hn : H[c];
+            }
+            Xl = X;
+            Hl = H[TD - 1];
+            HLp = HLn;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    // the cache: block (bi, bs) at slot (bi mod RC_CACHE, bs mod RC_CACHE); TC words per lane per 64-column
+    // stripe of the cache (RC_CACHE * 4 * CB)
+#pragma unroll
+    for (int p = 0; p < TD; p++) {
+        const uint4* src = reinterpret_cast<const uint4*>(stage + (p * 64 + lane) * SP);
+        uint4* dst = reinterpret_cast<uint4*>(r.tb) +
+                     ((long long)((bs % RC_CACHE) * TD + p) * r.TC + (bi % RC_CACHE) * 4 * CB) * 64 + lane;
+#pragma unroll
+        for (int d = 0; d < 4 * CB; d++) st16_sc1(dst + d * 64, src[d]);
+    }
+}
+
+template <int TD, int CB>
+__device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
+    const int lane = threadIdx.x & 63;
+    const int wave = sgpr((int)(threadIdx.x >> 6));
+    int8_t* stab = reinterpret_cast<int8_t*>(dyn);  // [K][32] sub'
+    for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x) stab[(q / r.K) * 32 + q % r.K] = (int8_t)r.subp[q];
+    __syncthreads();
+    if (wave >= r.workers) return;
+    uint8_t* wl = dyn + 1024 + wave * r.worker_bytes;
+    const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
+    const int worker = (blockIdx.x - 1) * r.workers + wave;
+    const int dbi = r.off[lane] >> 4, dbs = r.off[lane] & 15;
+    const int tile0 = (((r.m - 1) / RC_ROWS) << 16) | ((r.n - 1) / 64);  // the walk's first tile
+    unsigned idle = 0;
+    for (;;) {
+        if (sgpr((int)g_ld(r.pos + 1))) break;  // the walk has ended
+        const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
+        const int tile = pv ? (int)(pv - 1u) : tile0;
+        const int BI = tile >> 16, BS = (tile & 0xffff) / TD;
+        const int bi = BI - dbi, bs = BS - dbs;
+        const bool valid = bi >= 0 && bs >= 0 && bi < r.nbi && bs < r.nbs;
+        unsigned* fl = r.flags + (long long)(valid ? bi : 0) * r.nbs + (valid ? bs : 0);
+        const unsigned st = valid ? g_ld(fl) : ready;
+        unsigned long long freem = __ballot(valid && st < claimed);
+        bool did = false;
+        while (freem && !did) {
+            // workers start at different free blocks of the window (nearest first per worker)
+            const int npop = __popcll(freem);
+            unsigned long long mk = freem;
+            for (int x = worker % npop; x > 0; x--) mk &= mk - 1;
+            const int i = __builtin_ctzll(mk);
+            const int bi_i = __builtin_amdgcn_readlane(bi, i), bs_i = __builtin_amdgcn_readlane(bs, i);
+            unsigned exp = (unsigned)__builtin_amdgcn_readlane((int)st, i);
+            int won = 0;
+            if (lane == 0)
+                won = __hip_atomic_compare_exchange_strong(r.flags + (long long)bi_i * r.nbs + bs_i, &exp, claimed,
+                                                           __ATOMIC_RELAXED, __ATOMIC_RELAXED, AGENT);
+            if (sgpr(won)) {
+                rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the flag
+                if (lane == 0) g_st(r.flags + (long long)bi_i * r.nbs + bs_i, ready);
+                did = true;
+            }
+            freem &= ~(1ull << i);
+        }
+        if (did) {
+            idle = 0;
+            continue;
+        }
+        if (++idle > r.spin_limit) break;  // the walk's own bounded tile wait reports the failure
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+template <int CB, int TD>
+__global__ void __launch_bounds__(64 * WALK_WAVES) walk_rc_kernel(WalkArgs w, RcArgs r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    if (blockIdx.x == 0) walk_body<CB, true>(w, w.rng, reinterpret_cast<uint16_t*>(dyn));
+    else rc_server<TD, CB>(r, dyn);
+}
+
+template <int CB, int TD>
+static void launch_rc_one(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {
+    const size_t lds = std::max<size_t>((size_t)TP * TP * sizeof(uint16_t), 1024 + (size_t)r.workers * r.worker_bytes);
+    auto* fn = walk_rc_kernel<CB, TD>;
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<dim3(1 + nserv), dim3(64 * WALK_WAVES), lds, s>>>(w, r);
+}
+
+template <int CB>
+static void launch_rc_cb(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {
+    switch (r.TD) {
+        case 1: launch_rc_one<CB, 1>(s, w, r, nserv); break;
+        case 2: launch_rc_one<CB, 2>(s, w, r, nserv); break;
+        case 4: launch_rc_one<CB, 4>(s, w, r, nserv); break;
+        default: launch_rc_one<CB, 8>(s, w, r, nserv); break;
+    }
+}
+
+void launch_walk_rc(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {
+    if (w.CB == 1) launch_rc_cb<1>(s, w, r, nserv);
+    else if (w.CB == 2) launch_rc_cb<2>(s, w, r, nserv);
+    else launch_rc_cb<4>(s, w, r, nserv);
+}
+
+}  // namespace ga

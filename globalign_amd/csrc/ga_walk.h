@@ -8,6 +8,7 @@
 #include <type_traits>
 
 #include "ga_device.h"
+#include "ga_sync.h"
 
 namespace ga {
 
@@ -92,10 +93,31 @@ constexpr int NSLOT = TB4 * TB4;
 __device__ __forceinline__ int slot_of(int ti, int tj) { return (ti & (TB4 - 1)) * TB4 + (tj & (TB4 - 1)); }
 __device__ __forceinline__ int torus_of(int i, int j) { return ((i - 1) & (TP - 1)) * TP + ((j - 1) & (TP - 1)); }
 
+// Four 16-byte traceback words of a lane, 1 KiB apart (one 64-row tile of a column at one byte per cell), as
+// write-through-coherent (sc1) loads: the recompute walk's tiles are written by other workgroups of the
+// same launch with sc1 stores (ga_rcwalk.hip; MI355X_MICROARCH.md, inter-workgroup visibility)
+typedef unsigned wk_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ld4_sc1(const uint4* p, uint4 (&ch)[4]) {
+    wk_u4 c0, c1, c2, c3;
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off sc1\n\t"
+        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3)
+        : "v"(p)
+        : "memory");
+    ch[0] = make_uint4(c0.x, c0.y, c0.z, c0.w);
+    ch[1] = make_uint4(c1.x, c1.y, c1.z, c1.w);
+    ch[2] = make_uint4(c2.x, c2.y, c2.z, c2.w);
+    ch[3] = make_uint4(c3.x, c3.y, c3.z, c3.w);
+}
+
 // One loader wave decodes tile (ti, tj) into the torus: lane = column; the
 // tile's 64 rows of a column are 64/SPC whole 16-byte words of its stripe's
 // traceback stream (the general path; one-byte words use load_tile_b1).
-template <int CB>
+template <int CB, bool RC = false>
 __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
                           const uint8_t* lutF, int lane) {
     uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT;
@@ -106,11 +128,24 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, ui
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const int bj = colok ? w.b[j - 1] : 0xfe;
-    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC + ti * KW) * 64 + lane;
+    // RC: the recompute walk's tile cache (ga_rcwalk.hip): block row ti mod RC_CACHE, fill stripe tj / td mod RC_CACHE
+    const int tic = RC ? ti % RC_CACHE : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE) * w.rc_td + tj % w.rc_td : tj;
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tjc * w.TC + tic * KW) * 64 + lane;
     const int nq = min(KW, w.TC - ti * KW);
     uint4 ch[KW];
+    if constexpr (RC) {
+        // whole 1 KiB runs, 4 per call (the recompute walk's buffer has a tile of slack past its end)
 #pragma unroll
-    for (int k = 0; k < KW; k++) ch[k] = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < KW; k += 4) {
+            uint4 c4[4];
+            ld4_sc1(base + (long long)k * 64, c4);
+#pragma unroll
+            for (int u = 0; u < 4 && k + u < KW; u++) ch[k + u] = c4[u];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KW; k++) ch[k] = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -140,21 +175,32 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, ui
 // A lane's 64 cells are its four 16-byte words; it folds a_i == b_j into bit 7
 // of each word (SWAR zero-byte test on the staged a bytes; words use bits 0-6)
 // and decodes through a 256-entry table.
+template <bool RC = false>
 __device__ inline void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t* torus, uint8_t* sa, const uint16_t* lut,
-                             int lane) {
+                                    int lane) {
     uint16_t* dst = torus + (ti & (TB4 - 1)) * TT * TP + (tj & (TB4 - 1)) * TT + lane;
     const int i0 = ti * TT + 1;
     const int j = tj * TT + lane + 1;
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const unsigned bj = colok ? w.b[j - 1] : 0xfeu;
-    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tj * w.TC + ti * 4) * 64 + lane;
+    const int tic = RC ? ti % RC_CACHE : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE) * w.rc_td + tj % w.rc_td : tj;
+    const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tjc * w.TC + tic * 4) * 64 + lane;
     const int nq = w.TC - ti * 4;
     unsigned wv[16];
+    if constexpr (RC) {
+        uint4 c4[4];
+        ld4_sc1(base, c4);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint4 c = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
-        wv[4 * k] = c.x; wv[4 * k + 1] = c.y; wv[4 * k + 2] = c.z; wv[4 * k + 3] = c.w;
+        for (int k = 0; k < 4; k++) {
+            wv[4 * k] = c4[k].x; wv[4 * k + 1] = c4[k].y; wv[4 * k + 2] = c4[k].z; wv[4 * k + 3] = c4[k].w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 c = (colok && k < nq) ? base[(long long)k * 64] : make_uint4(0, 0, 0, 0);
+            wv[4 * k] = c.x; wv[4 * k + 1] = c.y; wv[4 * k + 2] = c.z; wv[4 * k + 3] = c.w;
+        }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): sa[] visible to this wave
     __builtin_amdgcn_wave_barrier();
@@ -193,13 +239,15 @@ __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
 
 // One walk by the whole workgroup (every wave returns from here once its role is done): the body of
 // walk_kernel, and of walk_chain_kernel once per alignment.  It initialises all of its LDS state.
-template <int CB>
-__device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng) {
+// torus: TP x TP u16 of LDS (the kernel's).  RC: the recompute walk (ga_rcwalk.hip): a tile
+// is loaded only once its block's flag says another workgroup has written its words (sc1 loads), the
+// helper publishes the walker's tile for those workgroups, and every tile wait is bounded.
+template <int CB, bool RC = false>
+__device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng, uint16_t* torus) {
     // the thread index through an opaque copy: in walk_chain_kernel nothing derived from it is hoisted
     // out of the loop over walks (it would stay live in VGPRs across every role's code)
     unsigned tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    __shared__ uint16_t torus[TP * TP];
     __shared__ __attribute__((aligned(16))) uint32_t rngbuf[RB];
     __shared__ uint32_t opsbuf[RB / 16];
     __shared__ uint16_t lut[256];
@@ -207,7 +255,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
     __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD_MAX][TT];
     __shared__ int tag[NSLOT];
     __shared__ int rtag[4];
-    __shared__ int cur_tile, walk_done, wD, ops_flushed;
+    __shared__ int cur_tile, walk_done, wD, ops_flushed, rc_timeout;
     __shared__ unsigned long long load_ticks;
     __shared__ int load_count;
     const int lane = tid & 63;
@@ -217,7 +265,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
     if (tid < NSLOT) tag[tid] = -1;
     if (tid < 4) rtag[tid] = -1;
     // a slab walk starts at dispatch D0: the rings start at its block
-    if (tid == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; }
+    if (tid == 0) { cur_tile = -1; walk_done = 0; wD = w.D0; ops_flushed = w.D0 >> 9; rc_timeout = 0; }
     if (CB == 1 && tid < 256)
         lut[tid] = (uint16_t)cell_shifts(sets_from_code(tid & 127u, 1, o), (tid >> 7) != 0);
     if (CB == 2 && tid < 128) {
@@ -273,10 +321,18 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         // ---------------- helper: tie-break table HBM -> LDS ring, levels LDS ring -> HBM ----------------
         const long long nblk = (w.nrng + 511) / 512;
         long long rl = w.D0 >> 9, fl = w.D0 >> 9;
+        int pub = -1;  // RC: the walker's tile last published for the recompute workgroups
         for (;;) {
             const int d = sgpr(__hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS));
             const int done = sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS));
             bool moved = false;
+            if constexpr (RC) {
+                const int cur = sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS));
+                if (cur >= 0 && cur != pub) {
+                    if (lane == 0) g_st(w.rc_pos, (unsigned)cur + 1u);  // 0: not yet published
+                    pub = cur;
+                }
+            }
             while (rl < nblk && rl < (d >> 9) + 4) {
                 const long long e0 = rl * 512 + lane * 8;
                 uint32_t* dst = rngbuf + (rl & 3) * 512 + lane * 8;
@@ -294,8 +350,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                 moved = true;
             }
             if (done && fl >= complete) break;
-            if (!moved) __builtin_amdgcn_s_sleep(8);
+            if (!moved) __builtin_amdgcn_s_sleep(RC ? 2 : 8);
         }
+        if (RC && lane == 0) g_st(w.rc_pos + 1, 1u);  // the recompute workgroups may end
         return;
     }
 
@@ -339,11 +396,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                     if (tg < 0) continue;
                     const int sl = li + nload * q, tti = tg >> 16, ttj = tg & 0xffff;
                     if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
+                    // RC: only once the tile's block has been recomputed (its words are then in memory)
+                    if (RC && sgpr((int)g_ld(w.rc_flags + (long long)tti * w.rc_nbs + ttj / w.rc_td)) != (int)w.rc_ready)
+                        continue;
                     if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_SEQ_CST, WGS);
                     if (!in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                    if (CB == 1) load_tile_b1(w, tti, ttj, torus, sa[li], lut, lane);
-                    else load_tile<CB>(w, tti, ttj, torus, sa[li], lut, lutF, lane);
+                    if (CB == 1) load_tile_b1<RC>(w, tti, ttj, torus, sa[li], lut, lane);
+                    else load_tile<CB, RC>(w, tti, ttj, torus, sa[li], lut, lutF, lane);
                     if (lane == 0) {
                         atomicAdd(&load_ticks, __builtin_amdgcn_s_memrealtime() - t0);
                         atomicAdd(&load_count, 1);
@@ -364,6 +424,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
     const int jend = w.handoff ? 5 : 2;  // reason when the walk reaches local column 0
     const int iend = w.vhandoff ? 6 : 1;  // ... and local row 0 (a traceback band with rows above it)
     int cti = -1, ctj = -1, nwait = 0, ntiles = 0, ndbg = 0;
+    unsigned rc_spins = 0;
+    bool rc_degenerate = false;
     const int maxh = w.maxh;
     unsigned long long t_tile = 0, t_ring = 0;  // time spent waiting (s_memrealtime ticks, 100 MHz)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -378,6 +440,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         while (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_ACQUIRE, WGS)) != tg) {
             __builtin_amdgcn_s_sleep(1);
             nwait++;
+            // RC: a tile that never comes (no recompute workgroup running) ends the walk on garbage with
+            // reason 7 instead of hanging; the host reports it
+            if (RC && ++rc_spins > (1u << 25)) {
+                rc_timeout = 1;
+                break;
+            }
         }
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
         t_tile += dt;
@@ -431,6 +499,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             sh = ((unsigned)sgpr(torus[torus_of(i, j)]) >> (5 * L)) & 31u;
         } else {
             // degenerate walk at row 0 / column 0 with Python index wrapping
+            // (RC: these cells' words may never have been recomputed; the host keeps such shapes off it)
+            if (RC) rc_degenerate = true;
             const int ri = i < 0 ? i + m + 1 : i, rj = j < 0 ? j + n + 1 : j;
             const int pa = (i - 1) < 0 ? i - 1 + m : i - 1, pb = (j - 1) < 0 ? j - 1 + n : j - 1;
             if (ri < 0 || rj < 0 || pa < 0 || pa >= m || pb < 0 || pb >= n) { reason = 4; break; }  // IndexError
@@ -587,6 +657,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         }
     }
     if (lane == 0) {
+        if (RC && (rc_timeout || rc_degenerate)) reason = 7;  // the recompute walk failed (host: GA_E_TIMEOUT)
         w.result[0] = D; w.result[1] = i; w.result[2] = j; w.result[3] = reason;
         w.result[4] = nwait; w.result[5] = ntiles;
         w.result[6] = (int)t_tile; w.result[7] = (int)t_ring;
@@ -601,7 +672,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
 
 template <int CB>
 __global__ void __launch_bounds__(64 * WALK_WAVES) walk_kernel(WalkArgs w) {
-    walk_body<CB>(w, w.rng);
+    __shared__ uint16_t torus[TP * TP];
+    walk_body<CB>(w, w.rng, torus);
 }
 
 // A slot's walk arguments, read from the kernel arguments at a run-time index (vector loads), made
@@ -640,6 +712,8 @@ __device__ __forceinline__ WalkArgs uniform_walk_args(const WalkArgs& s) {
     w.dbg = sgpr_ptr(s.dbg);
     w.skip_corners = sgpr(s.skip_corners);
     w.nloaders = sgpr(s.nloaders);
+    w.rc_flags = nullptr;
+    w.rc_pos = nullptr;
     return w;
 }
 
@@ -653,6 +727,7 @@ template <int CB>
 __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainArgs a) {
     __shared__ int go;
     __shared__ long long gnext;
+    __shared__ uint16_t torus[TP * TP];
     long long G = 0;
     for (int k = 0; k < a.count; k++) {
         int wait_fill = 0, wait_tab = 0;  // polls that found the fill / the entries not ready (diagnostics)
@@ -683,7 +758,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainAr
         if (!sgpr(go)) return;  // uniform: the walks' control flow and arguments stay scalar
         __threadfence();  // acquire: the slot's traceback words and boundary, written by fill k
         const WalkArgs w = uniform_walk_args(a.w[k % a.S]);
-        walk_body<CB>(w, a.tab + G);
+        walk_body<CB>(w, a.tab + G, torus);
         if (threadIdx.x == 0) {  // result[12..14]: this walk's wait before it started (ticks, polls)
             w.result[12] = (int)t_wait;
             w.result[13] = wait_fill;
