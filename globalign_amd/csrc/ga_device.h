@@ -105,7 +105,8 @@ struct RcArgs {
     int workers;           // waves per workgroup that recompute (the rest leave)
     int worker_bytes;      // LDS per worker
     unsigned spin_limit;   // idle polls before a worker gives up (the walk then reports its own timeout)
-    unsigned char off[64]; // window offsets (dbi << 4 | dbs) from the walker's block, nearest first
+    int nwin;              // window blocks (<= 64)
+    unsigned char off[64]; // window offsets (dbi << 4 | dbs) from the walker's block, likeliest first
 };
 
 // Pipelined walks in one launch (walk_chain_kernel): walk k uses w[k % S] with rng = tab + G_k.

@@ -723,6 +723,9 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         HIPCHK(c->stck.ensure(sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64));
         p.colck = c->colck.as<int2>();
         p.stck = c->stck.as<int2>();
+        // (timing experiments only: leave one kind of checkpoint out; the walk is then wrong)
+        if (getenv("GA_RC_DBG_NOCOL")) p.colck = nullptr;
+        if (getenv("GA_RC_DBG_NOST")) p.stck_every = -1;
     }
     p.subp = c->qp.as<int>();
     p.K = c->K;
@@ -1181,19 +1184,28 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     r.epoch = c->rc_epoch;
     r.pos = c->rc_pos.as<unsigned>();
     r.worker_bytes = ga::rc_worker_bytes(TD, CB, bd.rc_every);
+    // one worker per workgroup (one per CU) by default: C3 blocks 14.7 us against 16.5 at three per CU,
+    // the walker's tile waits 0.07 against 0.5 ms (tools/exp/r3_rc_diag.py)
     r.workers = std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
+    if (const char* e = getenv("GA_RC_WPW")) r.workers = std::max(1, std::min(r.workers, atoi(e)));
+    else r.workers = 1;
     r.spin_limit = 1u << 20;
     {
-        // the window: 8 x 8 blocks up-left of the walker's, nearest first (tile distance dbi + dbs * TD)
+        // the window: blocks up-left of the walker's (dbi block rows, dbs stripes), the path's likeliest
+        // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
+        // diagonal, dbi + dbs*TD + |dbi - dbs*TD|.  Only the first nwin are recomputed ahead (the walker's
+        // own 2 x 2 tiles always rank first); speculative blocks cost the workers' time and the claims.
         std::vector<std::pair<int, int>> off;
         for (int di = 0; di < 8; di++)
-            for (int dj = 0; dj < 8; dj++) off.push_back({di * 16 + dj, di + dj * TD});
+            for (int dj = 0; dj < 8; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
         std::stable_sort(off.begin(), off.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
             return x.second < y.second;
         });
         for (int k = 0; k < 64; k++) r.off[k] = (unsigned char)off[k].first;
+        r.nwin = 48;
+        if (const char* e = getenv("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
     }
-    int nserv = 24;
+    int nserv = 96;
     if (const char* e = getenv("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
     HIPCHK(hipEventRecord(wb.ev0, wb.stream));
     ga::launch_walk_rc(wb.stream, w, r, nserv);
@@ -2259,6 +2271,15 @@ int ga_debug_rng_chunked(const uint32_t* state, int64_t steps, int64_t chunk, ui
 
 // out6 = {tile wait spins, tiles entered, tile-wait ticks, ring-wait ticks, walker ticks (100 MHz),
 //         walker shader clocks / 16, loader busy ticks, tiles loaded}
+// Diagnostics of the last recompute walk: {blocks recomputed, their summed time in 100 MHz ticks,
+// recompute workers, checkpoint spacing}.
+int ga_debug_rc(ga_ctx* c, unsigned* out4) {
+    if (!c || !out4) return fail(GA_E_ARG, "null argument");
+    if (!c->rc_pos.p) return fail(GA_E_STATE, "no recompute walk ran");
+    HIPCHK(hipMemcpy(out4, c->rc_pos.p, sizeof(unsigned) * 4, hipMemcpyDeviceToHost));
+    return GA_OK;
+}
+
 int ga_debug_walk(ga_ctx* c, int* out5) {
     if (!c || !out5) return fail(GA_E_ARG, "null argument");
     out5[0] = c->walk_waits;

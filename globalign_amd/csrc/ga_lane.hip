@@ -393,7 +393,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         if constexpr (RC) {
             // lane 64-SUB+u holds row rlo+u of this stripe's right edge
             const int row = rlo + lane - (64 - SUB);
-            if (lane >= 64 - SUB && row >= 1 && row <= m) p.colck[(long long)s * (m + 1) + row] = make_int2(RH, RX);
+            if (p.colck != nullptr && lane >= 64 - SUB && row >= 1 && row <= m)
+                p.colck[(long long)s * (m + 1) + row] = make_int2(RH, RX);
         }
     };
     // traceback words: window w of 16 steps done -> aligned word w - 1 - lane/16 of every column (LkRot)
@@ -439,7 +440,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         if constexpr (RC) {
             // staircase checkpoint k after step k*E - 1: lane 0 has finished row k*E, lane l row k*E - l
             const int done = r0 + 2 * SUB;
-            if (done % p.stck_every == 0 && done < m) {
+            if (p.stck_every > 0 && done % p.stck_every == 0 && done < m) {
                 int2* ck = p.stck + ((long long)(done / p.stck_every - 1) * p.nstripes + s) * (TD + 1) * 64 + lane;
 #pragma unroll
                 for (int k = 0; k < TD; k++) ck[k * 64] = make_int2(H[k], Y[k]);

@@ -27,10 +27,12 @@ namespace ga {
 
 constexpr int RC_ROWS = 64;   // rows per block (one walker tile row)
 
-__host__ __device__ inline int rc_sp(int CB) { return 64 * CB + 16; }      // stage bytes per column (+16: banks)
+// stage bytes per column: rows t0-63 .. t0+nst (every row a lane visits in a block's steps, so the code
+// stores need no range test; only rows R0+1 .. R0+64 are read back), +16 against bank conflicts
+__host__ __device__ inline int rc_sp(int CB, int every) { return (((every + 136) * CB + 16) + 15) & ~15; }
 __host__ __device__ inline int rc_aw(int every) { return every + 256; }    // a-window dwords / edge-window rows
 int rc_worker_bytes(int TD, int CB, int every) {
-    return 64 * TD * rc_sp(CB) + 16 + rc_aw(every) * 4 + rc_aw(every) * 8;
+    return 64 * TD * rc_sp(CB, every) + rc_aw(every) * 4 + rc_aw(every) * 8;
 }
 
 __device__ __forceinline__ void st16_sc1(uint4* p, uint4 v) {
@@ -41,20 +43,20 @@ __device__ __forceinline__ void st16_sc1(uint4* p, uint4 v) {
 // Recompute block (bi, bs): rows 64*bi+1 .. 64*bi+64 of fill stripe bs, its traceback words into the cache.
 template <int TD, int CB>
 __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int bi, int bs, int lane) {
-    const int SP = rc_sp(CB), AW = rc_aw(r.stck_every);
+    const int SP = rc_sp(CB, r.stck_every), AW = rc_aw(r.stck_every);
     uint8_t* stage = wl;                                                  // [64*TD columns][SP]
-    uint32_t* awin = reinterpret_cast<uint32_t*>(wl + 64 * TD * SP + 16);  // dword i: a[base+i .. base+i+3]
+    uint32_t* awin = reinterpret_cast<uint32_t*>(wl + 64 * TD * SP);  // dword i: a[base+i .. base+i+3]
     int2* ewin = reinterpret_cast<int2*>(awin + AW);                      // left edge of rows t0+1 ..
     const int m = r.m, n = r.n, o = r.o;
     const int R0 = bi * RC_ROWS;
     const int nrow = min(RC_ROWS, m - R0);
     const int ck = R0 / r.stck_every;  // the staircase checkpoint above the block (0: row 0)
     const int t0 = ck * r.stck_every;
-    const int nst = ((R0 + nrow + 62) - t0 + 1 + 3) & ~3;  // steps, whole groups of 4 (lane 63 ends the block)
+    const int nst = ((R0 + nrow + 62) - t0 + 1 + 7) & ~7;  // steps, whole pairs of 4-step groups (lane 63 ends the block)
     const int base = t0 - 63;                               // a index of lane 63's row at step t0
     const int s = bs;
     const int j0 = s * 64 * TD, jl = j0 + lane * TD;
-    for (int i = lane; i < nst + 64; i += 64) {  // (a lane reads dwords up to nst + 59)
+    for (int i = lane; i < nst + 72; i += 64) {  // (a lane reads dwords up to nst + 67: one group ahead)
         uint32_t v = 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -64,7 +66,7 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
         awin[i] = v;
     }
     const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
-    for (int i = lane; i < nst; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
+    for (int i = lane; i < nst + 8; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
     int bcode[TD];
     int H[TD], Y[TD];
     int Xl = 0, HLp = 0;
@@ -92,13 +94,13 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     }
     int Hl = H[TD - 1];
     const unsigned op1 = (unsigned)o + 1u;
-    uint8_t* dummy = stage + 64 * TD * SP;
+    // this lane's code bytes: column c at stage + (lane*TD + c)*SP, row r at (r - t0 + 63)*CB
+    uint8_t* lst = stage + lane * TD * SP + (63 - t0) * CB;
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the windows written by this wave
     __builtin_amdgcn_wave_barrier();
-    for (int g = 0; g < nst; g += 4) {
-        const int t = t0 + g;
-        const uint32_t aw = awin[t - lane - base];  // this lane's a codes at steps t .. t+3
-        int sb[4][TD];
+    // the profile and edges of a group of 4 steps, read one group ahead
+    auto reads = [&](int g, int (&sb)[4][TD], int (&eh)[4], int (&ex)[4]) {
+        const uint32_t aw = awin[t0 + g - lane - base];  // this lane's a codes at steps t .. t+3
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int ac = (int)((aw >> (8 * u)) & 0xffu) * 32;
@@ -107,24 +109,27 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
         }
         const int4 e01 = *reinterpret_cast<const int4*>(ewin + g);
         const int4 e23 = *reinterpret_cast<const int4*>(ewin + g + 2);
-        const int eh[4] = {e01.x, e01.z, e23.x, e23.z}, ex[4] = {e01.y, e01.w, e23.y, e23.w};
+        eh[0] = e01.x; eh[1] = e01.z; eh[2] = e23.x; eh[3] = e23.z;
+        ex[0] = e01.y; ex[1] = e01.w; ex[2] = e23.y; ex[3] = e23.w;
+    };
+    auto group = [&](int g, const int (&sb)[4][TD], const int (&eh)[4], const int (&ex)[4], auto MK) {
+        constexpr bool MASKED = decltype(MK)::value;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int row = t + u - lane + 1;
-            const bool act = row >= 1;
-            const bool inr = row > R0 && row <= R0 + nrow;
-            int X = __builtin_amdgcn_update_dpp(ex[u], Xl, 0x138, 0xf, 0xf, false);   // h1'(row, left)
+            const int row = t0 + g + u - lane + 1;
+            const bool act = !MASKED || row >= 1;
+            int X = __builtin_amdgcn_update_dpp(ex[u], Xl, 0x138, 0xf, 0xf, false);  // h1'(row, left)
             const int HLn = __builtin_amdgcn_update_dpp(eh[u], Hl, 0x138, 0xf, 0xf, false);
             int Hd = HLp;
+            uint8_t* dst = lst + row * CB;
 #pragma unroll
             for (int c = 0; c < TD; c++) {
                 const int M = Hd + sb[u][c];
                 const int Hn = min(min(M, X), Y[c]);
                 const unsigned code = lk_code<CB>(M, X, Y[c], Hn, op1);
-                uint8_t* dst = inr ? stage + (lane * TD + c) * SP + (row - R0 - 1) * CB : dummy;
-                if constexpr (CB == 1) *dst = (uint8_t)code;
-                else if constexpr (CB == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)code;
-                else *reinterpret_cast<uint32_t*>(dst) = code;
+                if constexpr (CB == 1) dst[c * SP] = (uint8_t)code;
+                else if constexpr (CB == 2) *reinterpret_cast<uint16_t*>(dst + c * SP) = (uint16_t)code;
+                else *reinterpret_cast<uint32_t*>(dst + c * SP) = code;
                 const int Ho = Hn + o;
                 X = min(X, Ho);
                 Y[c] = act ? min(Y[c], Ho) : Y[c];
@@ -135,6 +140,18 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
             Hl = H[TD - 1];
             HLp = HLn;
         }
+    };
+    int sbA[4][TD], ehA[4], exA[4], sbB[4][TD], ehB[4], exB[4];
+    reads(0, sbA, ehA, exA);
+    // (row 0: lanes above row 1 keep their state for the first 64 steps)
+    const int gmask = ck == 0 ? 64 : 0;
+    for (int g = 0; g < nst; g += 8) {
+        reads(g + 4, sbB, ehB, exB);
+        if (g < gmask) group(g, sbA, ehA, exA, std::true_type{});
+        else group(g, sbA, ehA, exA, std::false_type{});
+        reads(g + 8, sbA, ehA, exA);
+        if (g + 4 < gmask) group(g + 4, sbB, ehB, exB, std::true_type{});
+        else group(g + 4, sbB, ehB, exB, std::false_type{});
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
@@ -142,7 +159,7 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     // stripe of the cache (RC_CACHE * 4 * CB)
 #pragma unroll
     for (int p = 0; p < TD; p++) {
-        const uint4* src = reinterpret_cast<const uint4*>(stage + (p * 64 + lane) * SP);
+        const uint4* src = reinterpret_cast<const uint4*>(stage + (p * 64 + lane) * SP + (R0 - t0 + 64) * CB);  // row R0+1
         uint4* dst = reinterpret_cast<uint4*>(r.tb) +
                      ((long long)((bs % RC_CACHE) * TD + p) * r.TC + (bi % RC_CACHE) * 4 * CB) * 64 + lane;
 #pragma unroll
@@ -160,7 +177,6 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     if (wave >= r.workers) return;
     uint8_t* wl = dyn + 1024 + wave * r.worker_bytes;
     const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
-    const int worker = (blockIdx.x - 1) * r.workers + wave;
     const int dbi = r.off[lane] >> 4, dbs = r.off[lane] & 15;
     const int tile0 = (((r.m - 1) / RC_ROWS) << 16) | ((r.n - 1) / 64);  // the walk's first tile
     unsigned idle = 0;
@@ -170,17 +186,14 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
         const int tile = pv ? (int)(pv - 1u) : tile0;
         const int BI = tile >> 16, BS = (tile & 0xffff) / TD;
         const int bi = BI - dbi, bs = BS - dbs;
-        const bool valid = bi >= 0 && bs >= 0 && bi < r.nbi && bs < r.nbs;
+        const bool valid = lane < r.nwin && bi >= 0 && bs >= 0 && bi < r.nbi && bs < r.nbs;
         unsigned* fl = r.flags + (long long)(valid ? bi : 0) * r.nbs + (valid ? bs : 0);
         const unsigned st = valid ? g_ld(fl) : ready;
         unsigned long long freem = __ballot(valid && st < claimed);
         bool did = false;
         while (freem && !did) {
-            // workers start at different free blocks of the window (nearest first per worker)
-            const int npop = __popcll(freem);
-            unsigned long long mk = freem;
-            for (int x = worker % npop; x > 0; x--) mk &= mk - 1;
-            const int i = __builtin_ctzll(mk);
+            // the likeliest free block first (the window is in priority order); a lost claim tries the next
+            const int i = __builtin_ctzll(freem);
             const int bi_i = __builtin_amdgcn_readlane(bi, i), bs_i = __builtin_amdgcn_readlane(bs, i);
             unsigned exp = (unsigned)__builtin_amdgcn_readlane((int)st, i);
             int won = 0;
@@ -188,9 +201,14 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
                 won = __hip_atomic_compare_exchange_strong(r.flags + (long long)bi_i * r.nbs + bs_i, &exp, claimed,
                                                            __ATOMIC_RELAXED, __ATOMIC_RELAXED, AGENT);
             if (sgpr(won)) {
+                const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
                 rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the flag
                 if (lane == 0) g_st(r.flags + (long long)bi_i * r.nbs + bs_i, ready);
+                if (lane == 0) {  // diagnostics: blocks recomputed, their total time (100 MHz ticks)
+                    atomicAdd(r.pos + 2, 1u);
+                    atomicAdd(r.pos + 3, (unsigned)(__builtin_amdgcn_s_memrealtime() - c0));
+                }
                 did = true;
             }
             freem &= ~(1ull << i);
