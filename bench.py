@@ -6,9 +6,10 @@
 
 Workloads (BASELINE.json configs, SURVEY 8d SplitMix64 inputs, resident in HBM):
   c3 (default at N=1): 100k x 100k DNA, match 2 / mismatch -3 / open -5 / ext -1, full traceback --
-                the config BASELINE's roofline target is quoted on.  A step is the whole
-                find_global_alignment DP (fill + tie-break table + walk + strings,
-                globaligner.py:258-302).  The N=1 line also carries "c4": one GPU's point of
+                the config BASELINE's roofline target is quoted on.  A step is ONE whole
+                find_global_alignment DP call (fill + tie-break table + walk + strings,
+                globaligner.py:258-302), steps run one after another with nothing overlapped; the
+                repeated-pair pipeline is reported beside it as an extra key.  The N=1 line also carries "c4": one GPU's point of
                 the C4 scaling curve.
   c4 (default at N>1): 1M x 1M DNA, same scoring, score only.  BASELINE's 1/2/4/8-GPU scaling
                 config: the SAME pair for every N (strong scaling), cut into N column slabs whose
@@ -77,9 +78,9 @@ MULTI_GPU_DEFAULT = "c4"
 # instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
 # (C3: the pipeline's lane-skewed traceback fill, fill_lane_kernel<4,4,1,8>; C4: the lane-skewed
 # score fill fill_lane_kernel<4,8,0,16>)
-TRAFFIC_FILES = {"c3": "r02/traffic_c3_lane.json", "c4": "r02/traffic_c4_lane.json"}
-VALU_FILES = {"c3": "r02/valu_c3_lane.json", "c4": "r02/valu_c4_lane.json"}
-VALU_MIX_FILES = {"c3": "r02/valu_mix_c3_lane.json", "c4": "r02/valu_mix_c4_lane.json"}
+TRAFFIC_FILES = {"c3": "r03/traffic_c3_rc.json", "c4": "r02/traffic_c4_lane.json"}
+VALU_FILES = {"c3": "r03/valu_c3_rc.json", "c4": "r02/valu_c4_lane.json"}
+VALU_MIX_FILES = {"c3": "r03/valu_mix_c3_rc.json", "c4": "r02/valu_mix_c4_lane.json"}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
 
@@ -287,10 +288,14 @@ def measure_single(wl, steps, warmup, pipelined=True):
 
         for _ in range(warmup):
             result = step()
+        first = result
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             result = step()
+            if wl["traceback"] and first is not None:
+                # every call starts from the same random state: the same alignment (checked, untimed cost ~us)
+                assert result[0] == first[0] and result[1] == first[1] and np.array_equal(result[3], first[3])
             tm = eng.timings()
             fill_l.append(tm["fill_ms"])
             walk_l.append(tm["walk_ms"] if wl["traceback"] else 0.0)
@@ -306,6 +311,7 @@ def measure_single(wl, steps, warmup, pipelined=True):
             out["mt_after"] = mt_after
             out["latency_ms"] = elapsed * 1e3 / steps
         out["mode"] = "one call per step"
+    out["fill_kind"] = eng.fill_kind()
     eng.close()
     cells = wl["m"] * wl["n"]
     out.update(elapsed=elapsed, cost=int(cost), cells=cells, value=cells * steps / elapsed,
@@ -329,7 +335,9 @@ def traceback_pin(workload, r):
 
 
 def single_line(args, workload, wl):
-    r = measure_single(wl, args.steps, args.warmup)
+    # the headline: consecutive single find_global_alignment-equivalent calls (ga_problem_align), nothing
+    # overlapped across steps (for C3-sized problems the recompute walk)
+    r = measure_single(wl, args.steps, args.warmup, pipelined=False)
     gold = golden_cost(wl.get("golden", workload))
     line = {
         "metric": METRIC,
@@ -347,17 +355,27 @@ def single_line(args, workload, wl):
         "config": {"workload": wl["desc"], "m": wl["m"], "n": wl["n"], "traceback": wl["traceback"],
                    "parallelism": "single GPU", "cost": r["cost"], "oracle_cost": gold,
                    "cost_matches_oracle": (r["cost"] == gold) if gold is not None else None},
-        "roofline": roofline(workload, wl, r["fill_ms"], per_step_ms=r["ms_per_step"] if r["mode"].startswith("pipelined")
-                             else None),
+        "roofline": roofline(workload, wl, r["fill_ms"]),
         "fill_ms": r["fill_ms"],
         "fill_cells_per_s": r["cells"] / (r["fill_ms"] * 1e-3),
     }
     if wl["traceback"]:
         line["walk_ms"] = r["walk_ms"]
+        line["walk_ns_per_step"] = r["walk_ms"] * 1e6 / max(len(r["aln"][1]), 1)
         line["host_tiebreak_ms"] = r["rng_ms"]
         line["latency_ms_per_alignment"] = r["latency_ms"]
         line["step_mode"] = r["mode"]
+        line["fill_kind"] = r.get("fill_kind")
         line["config"]["traceback_pin"] = traceback_pin(workload, r)
+        if not args.no_extra:
+            # the repeated-pair throughput mode (ga_problem_align_many: walk k beside fill k+1, stored words)
+            q = measure_single(wl, max(4, min(args.steps, 10)), 2, pipelined=True)
+            line["pipelined_repeated_pair"] = {
+                "value": q["value"], "unit": "cells/s", "ms_per_step": q["ms_per_step"], "steps": max(4, min(args.steps, 10)),
+                "cost_matches_oracle": (q["cost"] == gold) if gold is not None else None,
+                "traceback_pin": traceback_pin(workload, q),
+                "note": "consecutive alignments of the SAME pair with fills in flight beside the walks; not the "
+                        "headline (a single call cannot overlap)"}
     if workload == SINGLE_GPU_DEFAULT and not args.no_extra:
         # one GPU's point of BASELINE's C4 scaling curve (the same pair bench.py --gpus N slabs)
         w4 = WORKLOADS["c4"]

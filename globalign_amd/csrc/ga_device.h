@@ -102,6 +102,7 @@ struct RcArgs {
     unsigned* flags;       // [nbi][nbs]: < 2*epoch free, 2*epoch claimed, 2*epoch + 1 ready
     unsigned epoch;
     unsigned* pos;         // the walk's WalkArgs::rc_pos
+    int tile0;             // the walk's first tile (ti << 16 | tj), until it publishes one
     int workers;           // waves per workgroup that recompute (the rest leave)
     int worker_bytes;      // LDS per worker
     unsigned spin_limit;   // idle polls before a worker gives up (the walk then reports its own timeout)

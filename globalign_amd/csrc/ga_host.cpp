@@ -382,8 +382,9 @@ struct ga_ctx {
     // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
     DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
     unsigned rc_epoch = 0;
-    bool rc_used = false;  // the last ga_problem_align took the recompute path
+    bool rc_used = false;  // the last fill was the recompute path's (ga_problem_align or a slab's)
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
+    int rc_every_used = 64;
 };
 
 namespace {
@@ -1111,51 +1112,51 @@ bool rc_eligible(ga_ctx* c) {
     return c->m * c->n >= min_cells;
 }
 
-int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
-             int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
-    const double t0 = now_ms();
-    const int64_t m = c->m, n = c->n;
+// checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps; wider
+// spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per spacing
+int rc_every(ga_ctx* c) {
+    int every = 64;
+    if (const char* e = getenv("GA_RC_EVERY")) every = std::max(64, (atoi(e) / 32) * 32);
+    // memory: double the spacing until the states fit a budget (default 96 GB)
+    int64_t budget = (int64_t)96 << 30;
+    if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
+    const int64_t stripes = (c->n + 63) / 64;  // an upper bound at any TD: (TD + 1) / TD <= 2 per 64 columns
+    while ((c->m / every) * stripes * 2 * 512 > budget && every < 4096) every *= 2;
+    return every;
+}
+
+// The score-only checkpointing fill of the loaded problem or slab.
+int rc_fill(ga_ctx* c) {
     Band bd;
     bd.rc = true;
-    // checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps;
-    // wider spacing trades recompute steps for checkpoint memory (TD + 1) * 512 B per stripe per spacing
-    bd.rc_every = 64;
-    if (const char* e = getenv("GA_RC_EVERY")) bd.rc_every = std::max(64, (atoi(e) / 32) * 32);
-    {
-        // memory: halve the spacing's checkpoint bytes until they fit a budget (default 96 GB)
-        int64_t budget = (int64_t)96 << 30;
-        if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
-        const int64_t stripes = (n + 63) / 64;  // an upper bound at any TD: (TD + 1) / TD <= 2 per 64 columns
-        while ((m / bd.rc_every) * stripes * 2 * 512 > budget && bd.rc_every < 4096) bd.rc_every *= 2;
-    }
-    c->rc_used = true;
+    bd.rc_every = rc_every(c);
     if (int r = enqueue_fill(c, 0, bd)) return r;
-    const int TD = c->T;
-    c->rc_T = TD;
-    const int CB = c->CB;
+    c->rc_used = true;
+    c->rc_T = c->T;
+    c->rc_every_used = bd.rc_every;
+    return GA_OK;
+}
+
+// Launch the walk + recompute workgroups from walk state `st` on the walk buffers `wb` (its table already
+// uploaded), after rc_fill.
+int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
+    const int64_t m = c->m, n = c->n;
+    const int TD = c->rc_T, CB = c->CB;
     const int nbi = (int)((m + 63) / 64), nbs = c->nstripes;
     HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE * ga::RC_CACHE * TD * 64 * 64 * CB));
     const size_t nflags = (size_t)nbi * nbs;
     if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_epoch >= 0x7ffffff0u) {
         HIPCHK(c->rc_flags.ensure(nflags * sizeof(unsigned)));
-        HIPCHK(hipMemsetAsync(c->rc_flags.p, 0, c->rc_flags.cap, c->stream));
+        HIPCHK(hipMemsetAsync(c->rc_flags.p, 0, c->rc_flags.cap, wb.stream));
         c->rc_epoch = 0;
     }
     c->rc_epoch++;
     HIPCHK(c->rc_pos.ensure(16));
-    HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, c->stream));
-    // the tie-break table on the host while the device fills
-    RngTable R;
-    const double t1 = now_ms();
-    build_rng(mt_state, m + n + 1, R);
-    c->rng_ms = (float)(now_ms() - t1);
-    WalkBufs wb = ctx_walk_bufs(c);
+    HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, wb.stream));
     wb.tb = c->rc_tb.as<uint8_t>();
-    const int64_t ntab = (int64_t)R.tab.size();
-    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
-    ga::WalkArgs w = walk_args(c, ntab, WalkStart{m, n, 0, 0, 0, 1}, 0, -1, false, wb);
+    ga::WalkArgs w = walk_args(c, ntab, st, 0, -1, false, wb);
     w.TC = ga::RC_CACHE * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
-    w.nloaders = 14;                  // no L2 prefetcher (it would read blocks not yet recomputed)
+    w.nloaders = 14;                // no L2 prefetcher (it would read blocks not yet recomputed)
     w.rc_flags = c->rc_flags.as<unsigned>();
     w.rc_ready = 2u * c->rc_epoch + 1u;
     w.rc_nbs = nbs;
@@ -1167,10 +1168,11 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     r.subp = c->qp.as<int>();
     r.K = c->K;
     r.top = c->top.as<int2>() + c->col0;
-    r.left = c->left.as<int2>();
+    // the slab's left edge (another GPU's right edge, landed in full by now) or column 0
+    r.left = c->slab && c->col0 > 0 ? (c->halo_in_ext ? c->halo_in_ext : c->halo_in.as<int2>()) : c->left.as<int2>();
     r.colck = c->colck.as<int2>();
     r.stck = c->stck.as<int2>();
-    r.stck_every = bd.rc_every;
+    r.stck_every = c->rc_every_used;
     r.tb = c->rc_tb.as<uint8_t>();
     r.TC = w.TC;
     r.m = (int)m;
@@ -1183,7 +1185,8 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     r.flags = c->rc_flags.as<unsigned>();
     r.epoch = c->rc_epoch;
     r.pos = c->rc_pos.as<unsigned>();
-    r.worker_bytes = ga::rc_worker_bytes(TD, CB, bd.rc_every);
+    r.tile0 = (int)((((st.i - 1) / 64) << 16) | ((st.j - c->col0 - 1) / 64));  // the walk's first tile
+    r.worker_bytes = ga::rc_worker_bytes(TD, CB, r.stck_every);
     // one worker per workgroup (one per CU) by default: C3 blocks 14.7 us against 16.5 at three per CU,
     // the walker's tile waits 0.07 against 0.5 ms (tools/exp/r3_rc_diag.py)
     r.workers = std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
@@ -1211,8 +1214,37 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     ga::launch_walk_rc(wb.stream, w, r, nserv);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(wb.ev1, wb.stream));
+    return GA_OK;
+}
+
+// a slab's traceback fill (ga_slab_fill_launch): the same rule on the slab's own columns
+bool rc_slab_eligible(ga_ctx* c) {
+    const char* e = getenv("GA_RC");
+    const int mode = e ? atoi(e) : -1;
+    if (mode == 0 || c->qbytes != 1 || c->K > 32 || c->m < 256 || c->n < 256) return false;
+    if (mode == 1) return true;
+    int64_t min_cells = (int64_t)1 << 27;
+    if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
+    return c->m * c->n >= min_cells;
+}
+
+int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
+             int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const double t0 = now_ms();
+    const int64_t m = c->m, n = c->n;
+    if (int r = rc_fill(c)) return r;
+    // the tie-break table on the host while the device fills
+    RngTable R;
+    const double t1 = now_ms();
+    build_rng(mt_state, m + n + 1, R);
+    c->rng_ms = (float)(now_ms() - t1);
+    WalkBufs wb = ctx_walk_bufs(c);
+    const int64_t ntab = (int64_t)R.tab.size();
+    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    const WalkStart st0{m, n, 0, 0, 0, 1};
+    if (int r = rc_walk_launch(c, ntab, st0, wb)) return r;
     if (int rr = finish_fill(c, cost_out, nullptr)) return rr;
-    WalkStart st{m, n, 0, 0, 0, 1};
+    WalkStart st = st0;
     int reason = 0;
     int64_t len = 0;
     if (int rr = walk_segment(c, st, reason, a_chr, b_chr, oa, om, ob, cap, len, &wb)) return rr;
@@ -2117,6 +2149,13 @@ int ga_slab_fill_launch(ga_ctx* c, int32_t flags) {
     if (!c->slab) return fail(GA_E_STATE, "not a slab context");
     __atomic_store_n(&c->prog_host[0], 0u, __ATOMIC_SEQ_CST);
     __atomic_store_n(&c->prog_host[1], 0u, __ATOMIC_SEQ_CST);
+    c->rc_used = false;
+    if ((flags & GA_FILL_TRACEBACK) && rc_slab_eligible(c)) {
+        // the slab's traceback by recompute: checkpoints instead of m * n words
+        if (int r = rc_fill(c)) return r;
+        c->filled_tb = true;
+        return GA_OK;
+    }
     return enqueue_fill(c, flags & GA_FILL_TRACEBACK);
 }
 
@@ -2146,10 +2185,19 @@ int ga_slab_walk(ga_ctx* c, ga_walk_state* st, const char* a_chr, const char* b_
     if (st->j != c->col0 + c->n) return fail(GA_E_ARG, "walk state is not at this slab's right edge");
     if (st->i < 1 || st->i > c->m) return fail(GA_E_ARG, "walk row out of range");
     WalkStart ws{st->i, st->j, st->D, st->h, st->L, st->first};
-    if (int r = run_walk(c, c->walk_rng.tab.data(), (int64_t)c->walk_rng.tab.size(), ws)) return r;
     int reason = 0;
     int64_t len = 0;
-    if (int r = walk_segment(c, ws, reason, a_chr, b_chr, oa, om, ob, cap, len)) return r;
+    if (c->rc_used) {
+        WalkBufs wb = ctx_walk_bufs(c);
+        const int64_t ntab = (int64_t)c->walk_rng.tab.size();
+        HIPCHK(hipMemcpyAsync(wb.rng, c->walk_rng.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+        if (int r = rc_walk_launch(c, ntab, ws, wb)) return r;
+        if (int r = walk_segment(c, ws, reason, a_chr, b_chr, oa, om, ob, cap, len, &wb)) return r;
+        if (reason == 7) return fail(GA_E_TIMEOUT, "recompute walk: a tile was never recomputed");
+    } else {
+        if (int r = run_walk(c, c->walk_rng.tab.data(), (int64_t)c->walk_rng.tab.size(), ws)) return r;
+        if (int r = walk_segment(c, ws, reason, a_chr, b_chr, oa, om, ob, cap, len)) return r;
+    }
     st->i = ws.i;
     st->j = ws.j;
     st->D = ws.D;

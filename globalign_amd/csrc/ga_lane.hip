@@ -31,6 +31,10 @@
 #include "ga_lane.h"
 #include "ga_sync.h"
 
+#ifndef GA_LANE_LE
+#define GA_LANE_LE 13
+#endif
+
 namespace ga {
 
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
@@ -89,7 +93,6 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         const int2* rout = ring + nlive * RING;
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
         unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
-        bool in_wait = false;  // the last hand-off read found the writer behind: probe one row first
         // dword row r of code c: sub'(a_r .. a_r+3, c), rows outside 1..m zero.  A lane's window
         // may start up to 3 rows above row 1 (its first sub-chunk), so rows -2..0 are written too.
         auto put_dword = [&](int r) {
@@ -128,22 +131,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             }
             if (in_next < (unsigned)m && in_sent) {
                 const unsigned cap = min(min(lds_ld(&cnt[0]) + RING, (unsigned)m), in_next + in_win);
-                // while the writer is behind, one 8-byte probe of its next row per round trip instead of
-                // a 32-row read of mostly unwritten rows (HBM traffic of the polls)
-                bool probe_ok = true;
-                if (cap > in_next && in_wait) {
-                    const unsigned long long x = lane == 0 ? g_ld64(src + in_next + 1) : 0ull;
-                    probe_ok = __builtin_amdgcn_readfirstlane((int)(unsigned)x) != HAND_SENT;
-                }
-                if (cap > in_next && probe_ok) {
+                if (cap > in_next) {
+                    // one sc1 round trip per poll; while the writer is behind, its next 16 rows (the writer's
+                    // last compute wave stores a 16-step sub-chunk's rows at a time), else up to 64
                     const unsigned r = in_next + 1 + lane;
                     const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
                     const unsigned long long ok = __ballot(e1.x != HAND_SENT);
                     const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;
-                    // poll window: a reader waiting on the writer looks at the next 32 rows (one
-                    // sc1 round trip is ~1 us, and the chain produces a row every ~40-180 ns)
-                    in_win = k >= cap - in_next ? 64u : 32u;
-                    in_wait = k < cap - in_next;
+                    in_win = k >= cap - in_next ? 64u : 16u;
                     if (k > 0) {
                         if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
                         const unsigned hi = in_next + k;
@@ -164,7 +159,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                     moved = true;
                 }
             }
-            if (out_next < (unsigned)m) {
+            if (out_next < (unsigned)m && out_sent) {
+                // the last compute wave stores its right edge to the hand-off rows itself (sub_chunk): only
+                // its ring slots are freed here
+                const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
+                if (P > out_next) {
+                    lds_st(&cnt[2 * nlive], P);
+                    out_next = min(P, (unsigned)m);
+                    moved = true;
+                }
+            } else if (out_next < (unsigned)m) {
                 const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
                 const unsigned hi = min(min(P, (unsigned)m), out_next + 64);
                 if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
@@ -244,6 +248,12 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
     unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
+    // the workgroup's last compute wave writes the hand-off rows (not a slab's halo to another GPU, which
+    // the IO wave streams with its progress word)
+    const bool last_slab_w = g == p.nslabs - 1;
+    const bool hand_direct = w == nlive - 1 && !(last_slab_w && p.edge_out != nullptr);
+    int2* hand_out = p.hand + (long long)g * (m + 1);
+    const bool last_full = last_slab_w && p.n % (64 * TD) == 0;
     unsigned* cons_out = &cnt[2 * w + 2];
     unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
@@ -286,6 +296,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     unsigned pnext = *prod_in;  // the producer's counter, read a sub-chunk before it is needed
     // the banded traceback's score pass: the next checkpoint row any lane may still reach
     int next_ck = CKP ? p.ckpt_rows : 0x7fffffff;
+    // the step of a sub-chunk at which score-only waves await and read the next sub-chunk's edges
+    // (0: after the first step, as the traceback variants do)
+    constexpr int LE = (CB == 0 && !CKP && SUB == 16) ? GA_LANE_LE : 0;
     // lanes 64-SUB .. 63: the shift registers' rows of a sub-chunk
     unsigned long long out_mask = SUB == 16 ? 0xffff000000000000ull : 0xff00000000000000ull;
 
@@ -296,23 +309,37 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     auto sub_chunk = [&](int r0, int4 (&C)[NE], int4 (&Nx)[NE], uint32_t (&qc)[TD][NQ], uint32_t (&qx)[TD][NQ],
                          auto HALF) {
         constexpr int HB = decltype(HALF)::value * SUB;  // the sub-chunk's first step in its 16-step window
-        avail = sgpr_u(max(avail, pnext));
-        if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
+        if (!LE) {
+            avail = sgpr_u(max(avail, pnext));
+            if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
+        }
         if ((int)qavail < r0 + 2 * SUB) wait_ge(&cnt[LK_PRODQ], 0, qavail, r0 + 2 * SUB, 1);
         int eh[SUB], ex[SUB];
 #pragma unroll
         for (int k = 0; k < NE; k++) {
             eh[2 * k] = C[k].x; ex[2 * k] = C[k].y; eh[2 * k + 1] = C[k].z; ex[2 * k + 1] = C[k].w;
         }
-        auto loads = [&]() {
+        // the next sub-chunk's profile windows (the IO wave fills them far ahead) after the first step
+        auto qloads = [&]() {
             asm volatile("" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < NE; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK))[k];
             const unsigned idx = (unsigned)(r0 + SUB - lane) & qmask;
 #pragma unroll
             for (int k = 0; k < TD; k++)
 #pragma unroll
                 for (int d = 0; d < NQ; d++) qx[k][d] = pq[qb[k] + idx + 4 * d];
+            asm volatile("" ::: "memory");
+        };
+        // its left-edge rows and the producer's counter: after the first step, or (LE) only LE steps into
+        // the sub-chunk, awaiting them there -- the stripe then trails its left neighbour by SUB - LE
+        // steps less (the LDS read still lands SUB - LE steps before its first use)
+        auto eloads = [&]() {
+            asm volatile("" ::: "memory");
+            if (LE) {
+                avail = sgpr_u(max(avail, pnext));
+                if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < NE; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK))[k];
             pnext = __hip_atomic_load(prod_in, RLX, WGS);
             asm volatile("" ::: "memory");
         };
@@ -348,8 +375,15 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 }
             };
             one(std::integral_constant<int, 0>{});
-            loads();
-            LkUnroll<1, SUB>::run(one);
+            qloads();
+            if constexpr (LE > 0) {
+                LkUnroll<1, LE>::run(one);
+                eloads();
+                LkUnroll<LE, SUB>::run(one);
+            } else {
+                eloads();
+                LkUnroll<1, SUB>::run(one);
+            }
         };
         // wave-uniform: does any lane's window hold the next checkpoint row (lanes hold rows r0-62 .. r0+SUB)?
         const bool ckw = CKP && next_ck <= r0 + SUB;
@@ -390,6 +424,15 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             : "=&s"(saved)
             : "v"(oaddr), "v"(hx), "v"(pcl), "s"(om), "v"(cp)
             : "memory");
+        if (hand_direct) {
+            // the workgroup's right edge straight to its hand-off rows (agent-scope 8-byte stores, each row
+            // one untorn granule the next workgroup's IO wave polls for), 16 rows per sub-chunk
+            const int row = rlo + lane - (64 - SUB);
+            if (lane >= 64 - SUB && row >= 1 && row <= m) {
+                g_st64(hand_out + row, make_int2(RH, RX));
+                if (row == m && last_full) p.out_last[0] = RH;  // H'(m, n): the cost
+            }
+        }
         if constexpr (RC) {
             // lane 64-SUB+u holds row rlo+u of this stripe's right edge
             const int row = rlo + lane - (64 - SUB);

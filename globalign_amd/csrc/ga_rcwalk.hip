@@ -178,12 +178,11 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     uint8_t* wl = dyn + 1024 + wave * r.worker_bytes;
     const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
     const int dbi = r.off[lane] >> 4, dbs = r.off[lane] & 15;
-    const int tile0 = (((r.m - 1) / RC_ROWS) << 16) | ((r.n - 1) / 64);  // the walk's first tile
     unsigned idle = 0;
     for (;;) {
         if (sgpr((int)g_ld(r.pos + 1))) break;  // the walk has ended
         const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
-        const int tile = pv ? (int)(pv - 1u) : tile0;
+        const int tile = pv ? (int)(pv - 1u) : r.tile0;
         const int BI = tile >> 16, BS = (tile & 0xffff) / TD;
         const int bi = BI - dbi, bs = BS - dbs;
         const bool valid = lane < r.nwin && bi >= 0 && bs >= 0 && bi < r.nbi && bs < r.nbs;

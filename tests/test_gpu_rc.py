@@ -1,0 +1,130 @@
+"""GPU parity of the recompute walk: a score-only lane fill that leaves checkpoints (every
+stripe's right edge, staircase lane states every GA_RC_EVERY steps), then one launch in which workgroup 0
+walks while recompute workgroups rebuild the traceback words of the 64-row blocks ahead of it.  The result
+must equal the single-problem oracle exactly: cost, the three alignment strings, the final random state.
+GA_RC=1 forces the path at small sizes; the full-size C3 / C5 pins take it by default
+(test_gpu_parity.py::test_bench_workload_cost_matches_golden)."""
+import random
+
+import numpy as np
+import pytest
+
+from tests.conftest import splitmix_seq
+
+pytestmark = pytest.mark.gpu
+
+DNA = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+
+
+def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
+    from globalign_amd import _native
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    from tests.conftest import load_matrix
+    a1, a2, smat, cmat, gos, goc = transform.settings(dict(kw, seq_1=s1, seq_2=s2),
+                                                      blosum=load_matrix("BLOSUM62") if protein else None)
+    random.seed(seed)
+    mt = np.array(random.getstate()[1], dtype=np.uint32)
+    ref = core.align(a1, a2, cmat, goc, mt)
+    _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
+    tables = _native.CostTables(cmat2, goc2)
+    monkeypatch.setenv("GA_RC", "1")
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, str(v))
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(a1), tables.codes(a2), tables)
+        cost, strings, status, mt_after = eng.align(mt, a1, a2)
+        kind = eng.fill_kind()
+    finally:
+        eng.close()
+    assert kind[0] == "rc", kind  # the recompute path really ran
+    assert status == 0
+    assert int(cost) == ref["cost"]
+    assert tuple(strings) == tuple(ref["strings"])
+    assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+    return kind
+
+
+@pytest.mark.parametrize("m,n", [(256, 256), (300, 500), (1000, 1300), (777, 2049), (2049, 3000), (5000, 300),
+                                 (300, 5000), (4097, 4097)])
+def test_rc_dna_vs_oracle(monkeypatch, m, n):
+    _align(monkeypatch, splitmix_seq(m, 11, "dna"), splitmix_seq(n, 12, "dna"), DNA, seed=m + n)
+
+
+@pytest.mark.parametrize("td", [1, 2, 4, 8])
+def test_rc_stripe_widths_vs_oracle(monkeypatch, td):
+    """Every fill stripe width (64*TD columns): blocks of TD walker tiles, TD + 1 state pairs per lane."""
+    kind = _align(monkeypatch, splitmix_seq(3000, 21, "dna"), splitmix_seq(2500 + 64 * td, 22, "dna"), DNA, seed=td,
+                  env={"GA_LANE_COLS_PER_LANE": td})
+    assert kind[1] == td
+
+
+@pytest.mark.parametrize("every", [128, 256])
+def test_rc_checkpoint_spacing_vs_oracle(monkeypatch, every):
+    """Sparser staircase checkpoints: a block is recomputed from up to every + 126 steps above it."""
+    _align(monkeypatch, splitmix_seq(3000, 31, "dna"), splitmix_seq(3500, 32, "dna"), DNA, seed=every, env={"GA_RC_EVERY": every})
+
+
+@pytest.mark.parametrize("env", [{"GA_RC_SERVERS": 1, "GA_RC_WIN": 4},
+                                 {"GA_RC_SERVERS": 2, "GA_RC_WIN": 64, "GA_RC_WPW": 6},
+                                 {"GA_RC_SERVERS": 160, "GA_RC_WPW": 4}])
+def test_rc_worker_pools_vs_oracle(monkeypatch, env):
+    """One worker behind a narrow window, a few many-worker groups, many groups racing for claims."""
+    _align(monkeypatch, splitmix_seq(2500, 41, "dna"), splitmix_seq(2600, 42, "dna"), DNA, seed=7, env=env)
+
+
+@pytest.mark.parametrize("o", [7, 130])
+def test_rc_word_widths_vs_oracle(monkeypatch, o):
+    """Two- and four-byte traceback words (gap open >= 7, >= 128)."""
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-o, gap_extension_score=-1)
+    _align(monkeypatch, splitmix_seq(1500, 51, "dna"), splitmix_seq(1700, 52, "dna"), kw, seed=o)
+
+
+def test_rc_protein_blosum62_vs_oracle(monkeypatch):
+    kw = dict(scoring_mat_name="BLOSUM62", gap_open_score=-10)
+    _align(monkeypatch, splitmix_seq(1200, 3, "protein"), splitmix_seq(1400, 4, "protein"), kw, seed=3, protein=True)
+
+
+def test_rc_long_gap_runs_vs_oracle(monkeypatch):
+    """A pair whose path runs a long way along one edge: seq_2 = seq_1 plus 2000 extra columns (a
+    horizontal gap run the window must follow sideways), then seq_1 much longer than seq_2."""
+    a = splitmix_seq(2000, 61, "dna")
+    _align(monkeypatch, a, splitmix_seq(1000, 62, "dna") + a + splitmix_seq(1000, 63, "dna"), DNA, seed=61)
+    _align(monkeypatch, splitmix_seq(700, 64, "dna") + a + splitmix_seq(900, 65, "dna"), a, DNA, seed=62)
+
+
+def test_rc_similar_pair_vs_oracle(monkeypatch):
+    """Long diagonal match streaks (draw_two_random_seqs, 5 % divergence)."""
+    from globalign_amd.random_seqs import draw_two_random_seqs
+    orig = random.seed
+    monkeypatch.setattr(random, "seed", lambda a=None, version=2: orig(777 if a is None else a, version))
+    s1, s2 = draw_two_random_seqs(list("ACGT"), 3500, 3500, 3600, 3600, 0.05, 71, 72)
+    monkeypatch.setattr(random, "seed", orig)
+    _align(monkeypatch, s1, s2, DNA, seed=71)
+
+
+def test_rc_repeated_calls_reuse_buffers(monkeypatch):
+    """Consecutive calls on one context (new epochs over the same block flags and tile cache, shapes that
+    shrink and grow) stay exact."""
+    from globalign_amd import _native
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    monkeypatch.setenv("GA_RC", "1")
+    eng = _native.Engine(0)
+    try:
+        for k, (m, n) in enumerate([(2000, 2100), (900, 3000), (2000, 2100), (3100, 1200)]):
+            s1, s2 = splitmix_seq(m, 81 + k, "dna"), splitmix_seq(n, 91 + k, "dna")
+            a1, a2, smat, cmat, gos, goc = transform.settings(dict(DNA, seq_1=s1, seq_2=s2))
+            random.seed(k)
+            mt = np.array(random.getstate()[1], dtype=np.uint32)
+            ref = core.align(a1, a2, cmat, goc, mt)
+            _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **DNA)
+            tables = _native.CostTables(cmat2, goc2)
+            eng.load(tables.codes(a1), tables.codes(a2), tables)
+            cost, strings, status, mt_after = eng.align(mt, a1, a2)
+            assert eng.fill_kind()[0] == "rc"
+            assert status == 0 and int(cost) == ref["cost"] and tuple(strings) == tuple(ref["strings"])
+            assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+    finally:
+        eng.close()

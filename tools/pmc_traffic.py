@@ -14,7 +14,7 @@ def per_kernel(path):
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
         fam = "fill_kernel" if any(k in name for k in ("fill_kernel", "fill_diag_kernel", "fill_lane_kernel")) else \
-              "walk_kernel" if "walk_kernel" in name else None
+              "walk_kernel" if ("walk_kernel" in name or "walk_rc_kernel" in name) else None
         if fam is None:
             continue
         v = float(r["Counter_Value"])
