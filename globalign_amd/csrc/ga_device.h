@@ -47,6 +47,8 @@ struct FillArgs {
     int2* stck;               // staircase lane states after step k*stck_every - 1, k = 1 .. (m - 1) / stck_every:
                               //   [k - 1][nstripes][TD + 1][64]: (H'[c], h2'[c]) for c < TD, then (h1' carry, H' diag)
     int stck_every;           //   a multiple of 32 (a pair of 16-step sub-chunks)
+    int late;                 // lane fill, score only: late edge reads (one-round chains; ga_lane.hip LATE)
+    int hand_direct;          // lane fill: the last compute wave stores the hand-off rows (else the IO wave)
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),

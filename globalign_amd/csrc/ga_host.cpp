@@ -717,6 +717,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.ckpt_rows = bd.ckpt_rows;
     p.colck = nullptr;
     p.stck = nullptr;
+    // one round of lane workgroups (every stripe resident): the chain's lag counts, read edges late
+    p.late = c->lane && c->nslabs <= c->num_cu ? 1 : 0;
+    if (const char* e = getenv("GA_LANE_LATE")) p.late = atoi(e);
+    p.hand_direct = 1;
+    if (const char* e = getenv("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
     p.stck_every = bd.rc_every;
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / bd.rc_every, 1);

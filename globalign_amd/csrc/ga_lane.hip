@@ -53,7 +53,11 @@ size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
 // lane's whole state (its columns' H' and h2', the h1' it hands right, the diagonal H' it took from the
 // left) to p.stck: a staircase (lane l at row k*stck_every - l) from which any 64-row tile of the stripe
 // is recomputed with the same steps (ga_rcwalk.hip)
-template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false, bool RC = false>
+// LATE: score-only waves await and read the next sub-chunk's edges GA_LANE_LE steps into a sub-chunk
+// instead of after its first step (a stripe then trails its left neighbour by that many steps less, at ~3 %
+// more cycles per step): for one-round chains (C3, slabs), whose time is m steps plus every stripe's lag;
+// fills in rounds (C4 on one GPU) run uncoupled and keep the early reads
+template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false, bool RC = false, bool LATE = false>
 __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
@@ -159,7 +163,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                     moved = true;
                 }
             }
-            if (out_next < (unsigned)m && out_sent) {
+            if (out_next < (unsigned)m && out_sent && p.hand_direct) {
                 // the last compute wave stores its right edge to the hand-off rows itself (sub_chunk): only
                 // its ring slots are freed here
                 const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
@@ -251,7 +255,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     // the workgroup's last compute wave writes the hand-off rows (not a slab's halo to another GPU, which
     // the IO wave streams with its progress word)
     const bool last_slab_w = g == p.nslabs - 1;
-    const bool hand_direct = w == nlive - 1 && !(last_slab_w && p.edge_out != nullptr);
+    const bool hand_direct = p.hand_direct && w == nlive - 1 && !(last_slab_w && p.edge_out != nullptr);
     int2* hand_out = p.hand + (long long)g * (m + 1);
     const bool last_full = last_slab_w && p.n % (64 * TD) == 0;
     unsigned* cons_out = &cnt[2 * w + 2];
@@ -298,7 +302,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     int next_ck = CKP ? p.ckpt_rows : 0x7fffffff;
     // the step of a sub-chunk at which score-only waves await and read the next sub-chunk's edges
     // (0: after the first step, as the traceback variants do)
-    constexpr int LE = (CB == 0 && !CKP && SUB == 16) ? GA_LANE_LE : 0;
+    constexpr int LE = (CB == 0 && !CKP && SUB == 16 && LATE) ? GA_LANE_LE : 0;
     // lanes 64-SUB .. 63: the shift registers' rows of a sub-chunk
     unsigned long long out_mask = SUB == 16 ? 0xffff000000000000ull : 0xff00000000000000ull;
 
@@ -520,7 +524,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
     if constexpr (CB == 0 && !DBG && SUB == 16) {
         if (p.stck != nullptr) {
-            auto* fc = fill_lane_kernel<NWC, TD, 0, 16, false, false, true>;
+            auto* fc = fill_lane_kernel<NWC, TD, 0, 16, false, false, true, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
             return;
@@ -531,6 +535,14 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
             auto* fc = fill_lane_kernel<NWC, TD, CB, 8, false, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            return;
+        }
+    }
+    if constexpr (CB == 0 && SUB == 16) {
+        if (p.late) {
+            auto* fl = fill_lane_kernel<NWC, TD, 0, 16, DBG, false, false, true>;
+            (void)hipFuncSetAttribute((const void*)fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            fl<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
             return;
         }
     }

@@ -136,3 +136,20 @@ def test_global_aligner_devices_in_process(devices, m, n, seed, kw):
     assert random.getstate()[1] == tuple(int(x) for x in ref["mt_out"])
     r2 = globalign_amd.GlobalAligner(max_seq_len_prod=None, devices=devices, traceback=False, **kw).align(s1, s2)
     assert r2.cost == ref["cost"] and r2.seq_1_aligned is None
+
+
+@pytest.mark.parametrize("world,m,n,seed,band", [(2, 3000, 5000, 51, 512), (3, 2100, 4100, 52, 700)])
+def test_gpu_slabs_recompute_walk_match_oracle(world, m, n, seed, band, tmp_path, monkeypatch):
+    """Traceback across slabs through the recompute walk: each rank's slab
+    fill stores checkpoints only (no m x n words, so C4 traceback fits at N = 2 / 4), and each slab walk,
+    handed on right to left, recomputes the blocks ahead of it -- the leftmost slabs' stripe 0 from the
+    halo the left neighbour sent."""
+    monkeypatch.setenv("GA_RC", "1")
+    test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path)
+
+
+def test_global_aligner_devices_recompute_walk(monkeypatch):
+    """GlobalAligner(devices=[0, 0]) with the recompute walk on each slab."""
+    monkeypatch.setenv("GA_RC", "1")
+    test_global_aligner_devices_in_process([0, 0], 2600, 4200, 53, dict(match_score=2, mismatch_score=-3,
+                                                                        gap_open_score=-5, gap_extension_score=-1))
