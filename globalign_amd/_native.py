@@ -41,6 +41,7 @@ class EngineError(RuntimeError):
 EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_align_many", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
+    "ga_slab_link", "ga_enable_peer_access",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
     "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_ctx_wait_stream", "ga_ctx_stream_priority",
     "ga_last_kernel_ms", "ga_last_timings",
@@ -110,6 +111,8 @@ def load_library():
         L.ga_problem_set_slab.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), i64, i64]
         L.ga_slab_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
         L.ga_slab_bind_halos.argtypes = [vp, vp, vp]
+        L.ga_slab_link.argtypes = [vp, vp]
+        L.ga_enable_peer_access.argtypes = [C.c_int, C.c_int]
         L.ga_slab_walk_prepare.argtypes = [vp, pu32]
         L.ga_slab_walk.argtypes = [vp, C.POINTER(WalkState), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
                                    C.c_char_p, i64, pi64]
@@ -134,6 +137,10 @@ def _check(rc):
         if rc == -1:
             raise ValueError(msg)
         raise EngineError(f"globalign_amd engine error {rc}: {msg}")
+
+
+# a progress word's value once the fill writing it (or the relay feeding it) has given up (ga_sync.h)
+PROG_ABORT = 0xFFFFFFFF
 
 
 def device_count():
@@ -310,6 +317,10 @@ class Engine:
         """Use caller-owned (m+1) x int2 buffers (device or pinned host memory) as the slab's edges."""
         _check(self._L.ga_slab_bind_halos(self._h, C.c_void_p(halo_in_ptr), C.c_void_p(halo_out_ptr)))
 
+    def slab_link(self, right):
+        """Join this slab (left) to its right neighbour's engine device to device (ga_slab_link)."""
+        _check(self._L.ga_slab_link(self._h, right._h))
+
     def slab_launch(self, traceback=False):
         _check(self._L.ga_slab_fill_launch(self._h, GA_FILL_TRACEBACK if traceback else 0))
         self.slab_buffers()
@@ -321,7 +332,10 @@ class Engine:
 
     # progress words of the running slab fill (pinned host memory shared with the kernel)
     def out_progress(self):
-        return self._out_prog.value
+        v = self._out_prog.value
+        if v == PROG_ABORT:
+            raise EngineError("the slab fill gave up before its right edge was complete")
+        return v
 
     def set_in_progress(self, rows):
         self._in_prog.value = int(rows)

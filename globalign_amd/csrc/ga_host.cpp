@@ -338,6 +338,10 @@ struct ga_ctx {
     uint32_t* prog_dev = nullptr;
     int2* halo_in_ext = nullptr;   // caller-bound halo buffers (e.g. tensors RCCL sends from / receives into)
     int2* halo_out_ext = nullptr;
+    // caller-bound progress words (device-visible; e.g. on the reading GPU, written over xGMI by the
+    // writing GPU's fill): nullptr keeps prog_dev[0] / prog_dev[1]
+    uint32_t* in_prog_ext = nullptr;
+    uint32_t* out_prog_ext = nullptr;
     RngTable walk_rng;             // tie-break table of the global problem (slab walks)
     // pipelined repeated alignments (ga_problem_align_many): two slots of traceback words, walk
     // buffers and events; the walk runs on its own stream beside the next fill
@@ -381,6 +385,9 @@ struct ga_ctx {
     DevBuf dbg, wdbg;
     // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
     DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
+    // ga_slab_link: this slab's left edge + its progress word, uncached device memory on this GPU that
+    // the left neighbour's fill writes (over xGMI when it runs on another GPU)
+    DevBuf link;
     unsigned rc_epoch = 0;
     bool rc_used = false;  // the last fill was the recompute path's (ga_problem_align or a slab's)
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
@@ -739,7 +746,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.top = (bd.top ? bd.top : btop.as<int2>()) + c->col0;
     if (c->slab && c->col0 > 0) {
         p.left = c->halo_in_ext ? c->halo_in_ext : c->halo_in.as<int2>();
-        p.left_prog = c->prog_dev;  // [0]: halo_in rows
+        p.left_prog = c->in_prog_ext ? c->in_prog_ext : c->prog_dev;  // [0]: halo_in rows
     } else {
         p.left = bleft.as<int2>() + bd.r0;
         p.left_prog = nullptr;
@@ -749,7 +756,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.abort_word = fl + 1;
     p.tb = tb ? tbb.as<uint8_t>() : nullptr;
     p.out_last = ob.as<int>();
-    p.edge_prog = c->slab ? c->prog_dev + 1 : nullptr;  // [1]: halo_out rows
+    p.edge_prog = c->slab ? (c->out_prog_ext ? c->out_prog_ext : c->prog_dev + 1) : nullptr;  // [1]: halo_out rows
     p.edge_out = c->slab ? c->halo_out_ext : nullptr;
     p.full = full ? c->full.as<int>() : nullptr;
     p.m = (int)m;
@@ -763,6 +770,9 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.cols_per_lane = c->T;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
+    if (const char* e = getenv("GA_HALO_SPIN_LIMIT")) p.halo_spin_limit = (unsigned)std::max(1L, atol(e));  // (tests)
+    // a slab with a left neighbour: every wait of its fill is, in the end, a wait for that halo
+    if (c->slab && c->col0 > 0) p.spin_limit = std::max(p.spin_limit, p.halo_spin_limit);
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
@@ -1974,7 +1984,8 @@ void ga_ctx_destroy(ga_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
-                      &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt})
+                      &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt, &c->colck, &c->stck,
+                      &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->link})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     for (auto& sl : c->pipe) {
@@ -2114,6 +2125,7 @@ int ga_problem_set_slab(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b
     if (int r = check_ctx(c)) return r;
     c->slab = true;
     c->halo_in_ext = c->halo_out_ext = nullptr;
+    c->in_prog_ext = c->out_prog_ext = nullptr;
     c->walk_rng_ready = false;
     if (int r = load_problem(c, a, m, b, n, cs, nullptr, nullptr, col_begin, col_end)) return r;
     HIPCHK(c->halo_in.ensure(sizeof(int2) * (m + 1)));
@@ -2134,6 +2146,44 @@ int ga_slab_bind_halos(ga_ctx* c, void* halo_in, void* halo_out) {
     if (!c->slab) return fail(GA_E_STATE, "not a slab context");
     c->halo_in_ext = static_cast<int2*>(halo_in);
     c->halo_out_ext = static_cast<int2*>(halo_out);
+    return GA_OK;
+}
+
+int ga_slab_link(ga_ctx* left, ga_ctx* right) {
+    if (int r = check_ctx(left)) return r;
+    if (int r = check_ctx(right)) return r;
+    if (left == right || !left->slab || !right->slab) return fail(GA_E_STATE, "ga_slab_link needs two slab contexts");
+    if (left->m != right->m || left->col0 + left->n != right->col0)
+        return fail(GA_E_ARG, "ga_slab_link: the slabs are not neighbours of one problem");
+    if (left->device != right->device) {
+        // left's fill stores into right's memory
+        if (int r = ga_enable_peer_access(left->device, right->device)) return r;
+    }
+    HIPCHK(hipSetDevice(right->device));
+    const size_t hbytes = sizeof(int2) * (size_t)(right->m + 1);
+    right->link.uncached = true;
+    HIPCHK(right->link.ensure(hbytes + 256));
+    uint8_t* base = right->link.as<uint8_t>();
+    auto* prog = reinterpret_cast<uint32_t*>(base + hbytes);
+    // both fills are launched after this returns: the word starts at 0 rows
+    HIPCHK(hipMemset(prog, 0, 256));
+    right->halo_in_ext = reinterpret_cast<int2*>(base);
+    right->in_prog_ext = prog;
+    left->halo_out_ext = reinterpret_cast<int2*>(base);
+    left->out_prog_ext = prog;
+    return GA_OK;
+}
+
+int ga_enable_peer_access(int device, int peer) {
+    if (device == peer) return GA_OK;
+    int can = 0;
+    HIPCHK(hipDeviceCanAccessPeer(&can, device, peer));
+    if (!can) return fail(GA_E_HIP, "device " + std::to_string(device) + " cannot access device " + std::to_string(peer));
+    HIPCHK(hipSetDevice(device));
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(GA_E_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+    (void)hipGetLastError();  // clear a sticky "already enabled"
     return GA_OK;
 }
 

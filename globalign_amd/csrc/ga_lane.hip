@@ -153,7 +153,13 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 }
             } else if (in_next < (unsigned)m) {
                 const unsigned space = lds_ld(&cnt[0]) + RING;
-                const unsigned avail = src_prog ? min(s_ld(src_prog), (unsigned)m) : (unsigned)m;
+                const unsigned pv = src_prog ? s_ld(src_prog) : (unsigned)m;
+                if (pv == PROG_ABORT) {  // the left neighbour's fill gave up
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    g_st(p.abort_word, 1u);
+                    break;
+                }
+                const unsigned avail = min(pv, (unsigned)m);
                 const unsigned hi = min(min(space, avail), in_next + 64);
                 if (hi > in_next && (hi - in_next >= 16 || hi == avail)) {
                     const unsigned r = in_next + 1 + lane;
@@ -205,6 +211,8 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 spins = 0;
             }
         }
+        // gave up before the right edge was complete: tell the reader of the edge (the next slab's fill)
+        if (!out_sent && out_next < (unsigned)m && p.edge_prog != nullptr && lane == 0) s_prog_abort(p.edge_prog);
         return;
     }
     if (w >= nlive) return;

@@ -45,6 +45,11 @@ __device__ __forceinline__ void s_st64(int2* p, int2 v) {
     unsigned long long x = (unsigned long long)(unsigned)v.x | ((unsigned long long)(unsigned)v.y << 32);
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), x, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// the progress word's value once its writer has aborted (never a row count)
+constexpr unsigned PROG_ABORT = 0xffffffffu;
+__device__ __forceinline__ void s_prog_abort(unsigned* p) {
+    __hip_atomic_store(p, PROG_ABORT, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Bounded spin: returns false (and raises the abort word) after `limit` sleeps.
 __device__ __forceinline__ bool spin_ok(unsigned& spins, unsigned limit, unsigned* abort_word) {

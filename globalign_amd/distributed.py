@@ -29,9 +29,13 @@ engine built on the oracle.
 """
 import math
 import os
+import threading
 import time
 
 import numpy as np
+
+# a progress word's value once its writer gave up (ga_sync.h PROG_ABORT)
+PROG_ABORT = 0xFFFFFFFF
 
 
 def slab_bounds(n, world, align=512):
@@ -101,7 +105,6 @@ class Links:
 
 def stream_edges(dist, links, engine, halo_in, halo_out, m, band, timeout_s=600.0, poll_s=20e-6):
     """Exchange this rank's slab edges with its neighbours while its fill runs."""
-    import threading
     rank, world = links.rank, links.world
     bl = bands(m, band)
     errors = []
@@ -122,6 +125,10 @@ def stream_edges(dist, links, engine, halo_in, halo_out, m, band, timeout_s=600.
                 engine.set_in_progress(bl[k][1])
         except Exception as e:  # surfaced by the caller
             errors.append(e)
+            try:
+                engine.set_in_progress(PROG_ABORT)  # the local fill stops waiting for the edge
+            except Exception:
+                pass
 
     th = None
     if rank > 0:
@@ -268,41 +275,57 @@ def assemble(segs, state, cost, engine, seq_1, seq_2):
     return cost, (sa[::-1], sm[::-1], sb[::-1]), 0, mt_after
 
 
-def align_devices(devices, seq_1, seq_2, a_codes, b_codes, tables, mt_words, traceback=True, timeout_s=600.0):
+_device_engines = {}
+_device_engines_lock = threading.Lock()
+
+
+def device_engines(devices):
+    """The slab engines of GlobalAligner(devices=...), one context per listed device, kept for the process
+    (per thread: contexts are not thread-safe) so repeated calls reuse their buffers and linked halos."""
+    key = (tuple(devices), threading.get_ident())
+    with _device_engines_lock:
+        engines = _device_engines.get(key)
+        if engines is None:
+            engines = [GpuSlabEngine(d) for d in devices]
+            _device_engines[key] = engines
+        return engines
+
+
+def align_devices(devices, seq_1, seq_2, a_codes, b_codes, tables, mt_words, traceback=True, engines=None):
     """One problem over several GPUs of THIS process (GlobalAligner(devices=[...])): one context and one
-    column slab per device, the slab edges in pinned host memory that both neighbours map, and this
-    thread relaying each slab's right-edge progress word to its right neighbour while the fills run.
-    The same slab protocol as the one-process-per-GPU path (align_slabs) without a process group.
-    -> (cost, strings or None, status, mt_words_after or None)."""
-    import torch
+    column slab per device.  Neighbouring slabs are linked device to device (ga_slab_link): each slab's
+    left edge and its progress word live in uncached memory on its own GPU, and the left neighbour's
+    fill writes them directly, over xGMI, with system-scope stores while the reading fill polls the word
+    (DESIGN.md 7).  No host thread relays anything; a fill that gives up marks its edge aborted, so its
+    right neighbours stop too.  -> (cost, strings or None, status, mt_words_after or None)."""
     world = len(devices)
     m, n = len(a_codes), len(b_codes)
     edges = slab_bounds(n, world)
-    engines = [GpuSlabEngine(d) for d in devices]
-    halos = [torch.empty((m + 1, 2), dtype=torch.int32, pin_memory=True) for _ in range(world - 1)]
+    if engines is None:
+        engines = device_engines(devices)
     for k, eng in enumerate(engines):
         eng.load_slab(a_codes, b_codes, tables, edges[k], edges[k + 1])
-        eng.slab_bind_halos(halos[k - 1].data_ptr() if k > 0 else 0, halos[k].data_ptr() if k < world - 1 else 0)
+    for k in range(world - 1):
+        engines[k].slab_link(engines[k + 1])
     # left to right: a slab only ever waits on slabs launched before it (slabs sharing a GPU run in turn)
-    for eng in engines:
-        eng.slab_launch(traceback=traceback)
-    if traceback:
-        engines[-1].slab_walk_prepare(mt_words)  # the host tie-break table, while the fills run
-    relayed = [0] * (world - 1)
-    t0 = time.monotonic()
-    while any(r < m for r in relayed):
-        moved = False
-        for k in range(world - 1):
-            p = min(engines[k].out_progress(), m)
-            if p > relayed[k]:
-                engines[k + 1].set_in_progress(p)
-                relayed[k] = p
-                moved = True
-        if not moved:
-            if time.monotonic() - t0 > timeout_s:
-                raise TimeoutError(f"slab edges stalled at {relayed} of {m} rows")
-            time.sleep(20e-6)
-    costs = [eng.slab_finish() for eng in engines]
+    launched, costs, error = [], [], None
+    try:
+        for eng in engines:
+            eng.slab_launch(traceback=traceback)
+            launched.append(eng)
+        if traceback:
+            engines[-1].slab_walk_prepare(mt_words)  # the host tie-break table, while the fills run
+    except Exception as e:
+        error = e
+    # every launched fill is waited for, failed or not: a running fill writes into its right neighbour's
+    # context, which must outlive it
+    for eng in launched:
+        try:
+            costs.append(eng.slab_finish())
+        except Exception as e:
+            error = error or e
+    if error is not None:
+        raise error
     cost = costs[-1]
     if not traceback:
         return cost, None, 0, None
@@ -341,6 +364,9 @@ class GpuSlabEngine:
 
     def slab_bind_halos(self, in_ptr, out_ptr, halo_in=None, halo_out=None):
         self.eng.slab_bind_halos(in_ptr, out_ptr)
+
+    def slab_link(self, right):
+        self.eng.slab_link(right.eng)
 
     def order_after(self, stream):
         self.eng.wait_stream(stream)

@@ -49,8 +49,9 @@ class GlobalAligner:
     lifts the reference's m*n < 2e7 API cap (the device path is sized for
     100k x 100k and beyond); ``traceback=False`` returns the score only.
     ``devices=[0, 1, ...]`` cuts seq_2's columns into one slab per listed GPU
-    of this process (distributed.align_devices: the slab edges stream through
-    mapped host memory while the fills run, the walk is handed right to left);
+    of this process (distributed.align_devices: each slab's fill writes its right
+    edge straight into its neighbour's GPU memory over xGMI while both fills
+    run, the walk is handed right to left);
     the result is identical to the one-GPU result.  For one process per GPU
     use globalign_amd.distributed (torch.distributed / RCCL).
     """

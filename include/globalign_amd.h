@@ -127,6 +127,17 @@ int ga_slab_buffers(ga_ctx* ctx, void** halo_in, uint32_t** halo_in_prog, void**
  * input and right-edge output (e.g. tensors that RCCL receives into / sends
  * from); NULL keeps the context's own buffer. */
 int ga_slab_bind_halos(ga_ctx* ctx, void* halo_in, void* halo_out);
+/* Join two neighbouring slab contexts of ONE process (GlobalAligner(devices=[...])) device to device: the
+ * right context allocates its left edge (m + 1 int2 rows) and a progress word in uncached device memory
+ * on its own GPU, and the left context's fill writes both directly -- system-scope stores, over xGMI
+ * when the contexts sit on different GPUs (peer access is enabled here) -- while the right context's
+ * fill polls the word.  No host thread relays anything.  Call after ga_problem_set_slab on both
+ * contexts and before either fill is launched (it zeroes the word); launch left before right.
+ * Replaces the pinned-host halos + host relay of round 2 (reference: none -- the reference is
+ * single-threaded CPU code). */
+int ga_slab_link(ga_ctx* left, ga_ctx* right);
+/* Let `device` read and write `peer`'s memory (hipDeviceEnablePeerAccess); GA_OK if already enabled. */
+int ga_enable_peer_access(int device, int peer);
 /* Launch the slab fill asynchronously on the context's compute stream. */
 int ga_slab_fill_launch(ga_ctx* ctx, int32_t flags);
 /* Wait for the slab fill; returns H'(m, col_end) un-shifted (only meaningful on the last slab). */

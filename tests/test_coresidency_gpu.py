@@ -35,8 +35,18 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, traceback=False):
-    """-> dict(cost, all_done_while_waiting, waited_s, fill_still_waiting, priority)."""
+def _halo_copy(stream, dst, src, rows, blocks=64):
+    """ga_debug_halo_copy: an RCCL-shaped copy kernel (256 threads, 20 KB LDS, > 256 registers per lane)."""
+    import ctypes as C
+    from globalign_amd import _native
+    f = _native.load_library().ga_debug_halo_copy
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+    f.restype = C.c_int
+    assert f(stream, dst, src, rows, blocks) == 0
+
+
+def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, traceback=False, heavy=False):
+    """-> dict(cost, all_done_while_waiting, waited_s, fill_still_waiting, priority, kind)."""
     import torch
     from globalign_amd import _native
     seq_1, seq_2 = splitmix_seq(m, 31, "dna"), splitmix_seq(n, 32, "dna")
@@ -65,7 +75,10 @@ def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, tra
     for k, s in enumerate(streams):
         with torch.cuda.stream(s):
             if k == nstreams // 2:
-                torch.add(edge, 0, out=halo)  # the halo lands through an elementwise kernel
+                if heavy:
+                    _halo_copy(s.cuda_stream, halo.data_ptr(), edge.data_ptr(), m + 1)
+                else:
+                    torch.add(edge, 0, out=halo)  # the halo lands through an elementwise kernel
             x = torch.arange(1 << 16, device=dev, dtype=torch.int32)
             sinks.append(x * 3 + k)
             ev = torch.cuda.Event()
@@ -81,12 +94,17 @@ def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, tra
     waited = time.monotonic() - t0
     fill_stream = torch.cuda.ExternalStream(right.stream(), device=dev)
     still_waiting = not fill_stream.query()  # the fill kernel has not exited
+    right_priority = right.stream_priority()
     right.set_in_progress(m)  # release the fill in every case (no hang)
     cost = right.slab_finish()
     torch.cuda.synchronize()
     ok_sinks = all(int(s[5].item()) == 15 + k for k, s in enumerate(sinks))
+    kind = right.fill_kind()
+    left.close()
+    right.close()
     return dict(cost=cost, all_done_while_waiting=done and ok_sinks, waited_s=waited,
-                fill_still_waiting=still_waiting, priority=right.stream_priority(), seqs=(seq_1, seq_2))
+                fill_still_waiting=still_waiting, priority=right_priority, seqs=(seq_1, seq_2), kind=kind,
+                halo_ok=bool(torch.equal(halo, edge)), tables=tables)
 
 
 def oracle_cost(seq_1, seq_2):
@@ -105,3 +123,30 @@ def test_kernel_on_later_stream_runs_beside_waiting_slab_fill(traceback):
     assert r["all_done_while_waiting"], f"kernels on later streams did not run beside the waiting fill ({r})"
     assert r["fill_still_waiting"], "the slab fill finished before its halo was released"
     assert r["cost"] == oracle_cost(*r["seqs"])
+
+
+def test_rccl_shaped_kernel_runs_beside_c4_slab_fill(monkeypatch):
+    """The same at the occupancy of a C4 slab at N = 8 (1M x 125k per GPU): a 125 440-column
+    slab in 64 x 2-column lane stripes, 4 compute waves + 1 IO wave per workgroup, 245 workgroups (one per
+    CU on 245 of the 256 CUs), each holding its LDS rings and profile table.  The halo arrives through a
+    kernel shaped like RCCL's receive kernel (256 threads, 20 KB LDS, > 256 registers per lane), which
+    must start and finish while the fill waits.  The cost must equal the one-GPU fill's."""
+    from globalign_amd import _native
+    monkeypatch.setenv("GA_LANE_COLS_PER_LANE", "2")
+    monkeypatch.setenv("GA_FILL_NWC", "4")
+    monkeypatch.setenv("GA_FILL_MODE", "lane")
+    m, split, width = 20_000, 2048, 245 * 4 * 128
+    r = run_coresidency(m=m, n=split + width, split=split, heavy=True, deadline_s=20.0)
+    kind = r["kind"]
+    assert kind[0] == "lane" and kind[1] == 2 and kind[3] == 4 and kind[4] == 245, kind
+    assert r["all_done_while_waiting"], f"the RCCL-shaped kernel did not run beside the waiting fill ({r})"
+    assert r["fill_still_waiting"], "the slab fill finished before its halo was released"
+    assert r["halo_ok"]
+    eng = _native.Engine(0)
+    try:
+        seq_1, seq_2 = r["seqs"]
+        eng.load(r["tables"].codes(seq_1), r["tables"].codes(seq_2), r["tables"])
+        cost, _ = eng.fill(traceback=False)
+    finally:
+        eng.close()
+    assert r["cost"] == cost

@@ -153,3 +153,50 @@ def test_global_aligner_devices_recompute_walk(monkeypatch):
     monkeypatch.setenv("GA_RC", "1")
     test_global_aligner_devices_in_process([0, 0], 2600, 4200, 53, dict(match_score=2, mismatch_score=-3,
                                                                         gap_open_score=-5, gap_extension_score=-1))
+
+
+def test_linked_slabs_abort_propagates(monkeypatch):
+    """ga_slab_link's error path: of three linked slabs only the middle and right ones are launched, so the
+    middle fill's wait for its left edge runs out (a short GA_HALO_SPIN_LIMIT); it marks its right edge
+    aborted, and the right fill -- launched with the default ~30 s limit -- stops at once instead of
+    waiting that out.  Both finishes raise; the same contexts then align a problem exactly."""
+    import time
+    from globalign_amd import _native, distributed
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+    m, n = 3000, 6144
+    s1, s2 = splitmix_seq(m, 61, "dna"), splitmix_seq(n, 62, "dna")
+    _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
+    tables = _native.CostTables(cmat, goc)
+    a, b = tables.codes(s1), tables.codes(s2)
+    engines = [distributed.GpuSlabEngine(0) for _ in range(3)]
+    try:
+        edges = distributed.slab_bounds(n, 3)
+        for k, eng in enumerate(engines):
+            eng.load_slab(a, b, tables, edges[k], edges[k + 1])
+        engines[0].slab_link(engines[1])
+        engines[1].slab_link(engines[2])
+        monkeypatch.setenv("GA_HALO_SPIN_LIMIT", str(1 << 16))
+        engines[1].slab_launch(traceback=False)
+        monkeypatch.delenv("GA_HALO_SPIN_LIMIT")
+        t0 = time.monotonic()
+        engines[2].slab_launch(traceback=False)
+        with pytest.raises(_native.EngineError):
+            engines[1].slab_finish()
+        with pytest.raises(_native.EngineError):
+            engines[2].slab_finish()
+        assert time.monotonic() - t0 < 10.0
+        # the contexts recover: a full linked alignment on them
+        a1, a2, _, cmat_o, _, goc_o = transform.settings(dict(kw, seq_1=s1, seq_2=s2))
+        random.seed(5)
+        ref = core.align(a1, a2, cmat_o, goc_o, core.mt_state_array())
+        random.seed(5)
+        mt = np.array(random.getstate()[1], dtype=np.uint32)
+        cost, strings, status, mt_after = distributed.align_devices([0, 0, 0], s1, s2, a, b, tables, mt,
+                                                                    engines=engines)
+        assert status == 0 and cost == ref["cost"] and tuple(strings) == tuple(ref["strings"])
+        assert np.asarray(mt_after, dtype=np.uint32).tolist() == [int(x) for x in ref["mt_out"]]
+    finally:
+        for eng in engines:
+            eng.eng.close()
