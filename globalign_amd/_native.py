@@ -41,7 +41,7 @@ class EngineError(RuntimeError):
 EXPORTS = [
     "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_align_many", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
-    "ga_slab_link", "ga_enable_peer_access",
+    "ga_slab_link", "ga_slab_link_export", "ga_slab_link_import", "ga_enable_peer_access",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
     "ga_stream_wait_ge", "ga_stream_write", "ga_ctx_stream", "ga_ctx_wait_stream", "ga_ctx_stream_priority",
     "ga_last_kernel_ms", "ga_last_timings",
@@ -112,6 +112,8 @@ def load_library():
         L.ga_slab_buffers.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)]
         L.ga_slab_bind_halos.argtypes = [vp, vp, vp]
         L.ga_slab_link.argtypes = [vp, vp]
+        L.ga_slab_link_export.argtypes = [vp, C.c_char_p]
+        L.ga_slab_link_import.argtypes = [vp, C.c_char_p]
         L.ga_enable_peer_access.argtypes = [C.c_int, C.c_int]
         L.ga_slab_walk_prepare.argtypes = [vp, pu32]
         L.ga_slab_walk.argtypes = [vp, C.POINTER(WalkState), C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
@@ -320,6 +322,18 @@ class Engine:
     def slab_link(self, right):
         """Join this slab (left) to its right neighbour's engine device to device (ga_slab_link)."""
         _check(self._L.ga_slab_link(self._h, right._h))
+
+    def slab_link_export(self):
+        """This (right) slab's side of a cross-process link -> the 64-byte IPC handle of its edge buffer."""
+        buf = C.create_string_buffer(64)
+        _check(self._L.ga_slab_link_export(self._h, buf))
+        return buf.raw
+
+    def slab_link_import(self, handle):
+        """Map the right neighbour's edge buffer (its slab_link_export bytes) as this slab's right edge."""
+        if len(handle) != 64:
+            raise ValueError("an IPC handle has 64 bytes")
+        _check(self._L.ga_slab_link_import(self._h, bytes(handle)))
 
     def slab_launch(self, traceback=False):
         _check(self._L.ga_slab_fill_launch(self._h, GA_FILL_TRACEBACK if traceback else 0))

@@ -11,26 +11,25 @@
 
 namespace {
 
-constexpr int HC_ROWS = 2560;  // 20 KB of int2 staging
-constexpr int HC_KEEP = 272;   // live registers beside the copy's own
-
-__global__ __launch_bounds__(256, 1) void halo_copy_kernel(int2* dst, const int2* src, long long rows, int salt) {
-    __shared__ int2 stage[HC_ROWS];
-    int keep[HC_KEEP];
+// THREADS threads, ROWS int2 of LDS staging, KEEP registers kept live beside the copy's own
+template <int THREADS, int ROWS, int KEEP>
+__global__ __launch_bounds__(THREADS, 1) void halo_copy_kernel(int2* dst, const int2* src, long long rows, int salt) {
+    __shared__ int2 stage[ROWS];
+    int keep[KEEP];
 #pragma unroll
-    for (int k = 0; k < HC_KEEP; k++) {
+    for (int k = 0; k < KEEP; k++) {
         keep[k] = salt * (k + 1) + (int)threadIdx.x;
         asm volatile("" : "+v"(keep[k]));
     }
-    for (long long r0 = (long long)blockIdx.x * HC_ROWS; r0 < rows; r0 += (long long)gridDim.x * HC_ROWS) {
-        for (int i = threadIdx.x; i < HC_ROWS && r0 + i < rows; i += blockDim.x) stage[i] = src[r0 + i];
+    for (long long r0 = (long long)blockIdx.x * ROWS; r0 < rows; r0 += (long long)gridDim.x * ROWS) {
+        for (int i = threadIdx.x; i < ROWS && r0 + i < rows; i += blockDim.x) stage[i] = src[r0 + i];
         __syncthreads();
-        for (int i = threadIdx.x; i < HC_ROWS && r0 + i < rows; i += blockDim.x) dst[r0 + i] = stage[i];
+        for (int i = threadIdx.x; i < ROWS && r0 + i < rows; i += blockDim.x) dst[r0 + i] = stage[i];
         __syncthreads();
     }
     int acc = 0;
 #pragma unroll
-    for (int k = 0; k < HC_KEEP; k++) {
+    for (int k = 0; k < KEEP; k++) {
         asm volatile("" : "+v"(keep[k]));
         acc ^= keep[k];
     }
@@ -39,9 +38,19 @@ __global__ __launch_bounds__(256, 1) void halo_copy_kernel(int2* dst, const int2
 
 }  // namespace
 
-extern "C" int ga_debug_halo_copy(void* stream, void* dst, const void* src, int64_t rows, int32_t blocks) {
-    if (!dst || !src || rows < 0 || blocks < 1) return GA_E_ARG;
-    hipLaunchKernelGGL(halo_copy_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       static_cast<int2*>(dst), static_cast<const int2*>(src), (long long)rows, 3);
+// variant 0: 256 threads, 20 KB LDS, ~280 registers per lane (the shape round 2's review asked for);
+// variant 1: 512 threads, 37 664 B LDS, 256 VGPRs -- the gfx950 code object of RCCL 7.2's
+// ncclDevKernel_Generic_4 (librccl.so metadata: vgpr_count 256, group_segment_fixed_size 37664,
+// max_flat_workgroup_size 512), which at 512 threads needs a CU of its own
+extern "C" int ga_debug_halo_copy(void* stream, void* dst, const void* src, int64_t rows, int32_t blocks,
+                                  int32_t variant) {
+    if (!dst || !src || rows < 0 || blocks < 1 || variant < 0 || variant > 1) return GA_E_ARG;
+    auto* d = static_cast<int2*>(dst);
+    auto* sp = static_cast<const int2*>(src);
+    auto st = static_cast<hipStream_t>(stream);
+    if (variant == 0)
+        hipLaunchKernelGGL((halo_copy_kernel<256, 2560, 272>), dim3(blocks), dim3(256), 0, st, d, sp, (long long)rows, 3);
+    else
+        hipLaunchKernelGGL((halo_copy_kernel<512, 4708, 236>), dim3(blocks), dim3(512), 0, st, d, sp, (long long)rows, 3);
     return hipGetLastError() == hipSuccess ? GA_OK : GA_E_HIP;
 }

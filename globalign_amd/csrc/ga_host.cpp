@@ -388,6 +388,9 @@ struct ga_ctx {
     // ga_slab_link: this slab's left edge + its progress word, uncached device memory on this GPU that
     // the left neighbour's fill writes (over xGMI when it runs on another GPU)
     DevBuf link;
+    // ga_slab_link_import: the right neighbour's link buffer, mapped from another process
+    void* peer_link = nullptr;
+    char peer_handle[64] = {};
     unsigned rc_epoch = 0;
     bool rc_used = false;  // the last fill was the recompute path's (ga_problem_align or a slab's)
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
@@ -454,7 +457,15 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T
         const char* e = getenv("GA_LANE_WG_PER_CU");
         return e ? std::max(1, std::min(2, atoi(e))) : 1;
     }();
-    const int64_t cus = c->num_cu * wpc;
+    int64_t cus = c->num_cu * wpc;
+    // A slab whose edge another kernel (an RCCL receive or send) must move WHILE the fill runs: keep one CU
+    // of every shader engine (8 CUs) free and every workgroup resident.  A kernel launched beside the fill
+    // places each of its workgroups on a CU of one shader engine, round robin, and waits there: measured
+    // (tools/exp/r3_cores.py), an RCCL-shaped kernel starts beside 224 fill workgroups on 256 CUs, not
+    // beside 228.  Linked edges (ga_slab_link / _import: the fill stores them itself) need no room.
+    const bool coresident = c->slab && ((c->col0 > 0 && !c->in_prog_ext) ||
+                                        (c->col0 + c->n < c->n_global && !c->out_prog_ext));
+    if (coresident) cus = c->num_cu - c->num_cu / 8;
     // Rounds: with 4-wave workgroups, one per CU, more stripes than 4 per CU run in rounds of workgroups.
     // A later round starts as the first finish, on left edges long written, so it runs uncoupled; the
     // chain then takes R*m + skew steps at the 1-wave step cost.  Not for a slab with a right neighbour
@@ -475,7 +486,7 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T
             if (force_N ? force_N != nwc : (c->nwc_req == 4 || c->nwc_req == 8) && nwc != c->nwc_req) continue;
             if (tb && c->CB == 4 && nwc == 8) continue;
             const int64_t rounds = (ns + nwc * cus - 1) / (nwc * cus);
-            if (rounds > 1 && (nwc == 8 || right_nb || tb)) continue;  // 8-wave workgroups: all resident
+            if (rounds > 1 && (nwc == 8 || right_nb || tb || coresident)) continue;  // 8-wave workgroups: all resident
             const double step = nwc == 4 ? cyc1[ti] : 2.1 * cyc1[ti];
             const double t = ((double)rounds * (double)c->m + 74.0 * (double)ns) * step;
             if (!bestT || t < best) {
@@ -1988,6 +1999,7 @@ void ga_ctx_destroy(ga_ctx* c) {
                       &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->link})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
+    if (c->peer_link) (void)hipIpcCloseMemHandle(c->peer_link);
     for (auto& sl : c->pipe) {
         for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result, &sl.GVp, &sl.GHp,
                           &sl.top, &sl.left, &sl.bnd_row, &sl.bnd_col, &sl.meta, &sl.bscr})
@@ -2149,6 +2161,22 @@ int ga_slab_bind_halos(ga_ctx* c, void* halo_in, void* halo_out) {
     return GA_OK;
 }
 
+// the right slab's side of a link: its left edge (m + 1 int2 rows) + progress word in uncached memory on
+// its own GPU, bound as its halo_in / in_prog; the word zeroed (before any writer is launched)
+static int link_alloc(ga_ctx* right, uint8_t** base_out) {
+    HIPCHK(hipSetDevice(right->device));
+    const size_t hbytes = sizeof(int2) * (size_t)(right->m + 1);
+    right->link.uncached = true;
+    HIPCHK(right->link.ensure(hbytes + 256));
+    uint8_t* base = right->link.as<uint8_t>();
+    auto* prog = reinterpret_cast<uint32_t*>(base + hbytes);
+    HIPCHK(hipMemset(prog, 0, 256));
+    right->halo_in_ext = reinterpret_cast<int2*>(base);
+    right->in_prog_ext = prog;
+    *base_out = base;
+    return GA_OK;
+}
+
 int ga_slab_link(ga_ctx* left, ga_ctx* right) {
     if (int r = check_ctx(left)) return r;
     if (int r = check_ctx(right)) return r;
@@ -2159,18 +2187,43 @@ int ga_slab_link(ga_ctx* left, ga_ctx* right) {
         // left's fill stores into right's memory
         if (int r = ga_enable_peer_access(left->device, right->device)) return r;
     }
-    HIPCHK(hipSetDevice(right->device));
-    const size_t hbytes = sizeof(int2) * (size_t)(right->m + 1);
-    right->link.uncached = true;
-    HIPCHK(right->link.ensure(hbytes + 256));
-    uint8_t* base = right->link.as<uint8_t>();
-    auto* prog = reinterpret_cast<uint32_t*>(base + hbytes);
-    // both fills are launched after this returns: the word starts at 0 rows
-    HIPCHK(hipMemset(prog, 0, 256));
-    right->halo_in_ext = reinterpret_cast<int2*>(base);
-    right->in_prog_ext = prog;
+    uint8_t* base = nullptr;
+    if (int r = link_alloc(right, &base)) return r;
     left->halo_out_ext = reinterpret_cast<int2*>(base);
-    left->out_prog_ext = prog;
+    left->out_prog_ext = reinterpret_cast<uint32_t*>(base + sizeof(int2) * (size_t)(right->m + 1));
+    return GA_OK;
+}
+
+int ga_slab_link_export(ga_ctx* right, void* handle_out) {
+    if (int r = check_ctx(right)) return r;
+    if (!handle_out) return fail(GA_E_ARG, "null argument");
+    if (!right->slab || right->col0 == 0) return fail(GA_E_STATE, "ga_slab_link_export needs a slab with a left neighbour");
+    uint8_t* base = nullptr;
+    if (int r = link_alloc(right, &base)) return r;
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, base));
+    std::memcpy(handle_out, &h, sizeof(h));
+    return GA_OK;
+}
+
+int ga_slab_link_import(ga_ctx* left, const void* handle) {
+    if (int r = check_ctx(left)) return r;
+    if (!handle) return fail(GA_E_ARG, "null argument");
+    if (!left->slab || left->col0 + left->n >= left->n_global)
+        return fail(GA_E_STATE, "ga_slab_link_import needs a slab with a right neighbour");
+    if (!left->peer_link || std::memcmp(left->peer_handle, handle, sizeof(left->peer_handle)) != 0) {
+        if (left->peer_link) (void)hipIpcCloseMemHandle(left->peer_link);
+        left->peer_link = nullptr;
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handle, sizeof(h));
+        void* p = nullptr;
+        HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        left->peer_link = p;
+        std::memcpy(left->peer_handle, handle, sizeof(left->peer_handle));
+    }
+    auto* base = static_cast<uint8_t*>(left->peer_link);
+    left->halo_out_ext = reinterpret_cast<int2*>(base);
+    left->out_prog_ext = reinterpret_cast<uint32_t*>(base + sizeof(int2) * (size_t)(left->m + 1));
     return GA_OK;
 }
 

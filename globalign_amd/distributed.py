@@ -3,7 +3,13 @@
 One process per GPU (``torch.distributed``; backend ``nccl`` = RCCL over xGMI on
 ROCm).  seq_2's columns are cut into contiguous slabs, one per rank.  Every
 rank runs its slab's fill as ONE kernel launch; the wavefront crosses a slab
-boundary through a single column of (H', h1') pairs, streamed in row bands:
+boundary through a single column of (H', h1') pairs.  By default (edge_mode
+"ipc") rank r+1 allocates that column and a progress word in uncached memory
+on its GPU and hands rank r a HIP IPC handle to it; rank r's fill stores the
+rows and raises the word itself, over xGMI, while rank r+1's fill polls it --
+no host thread, no RCCL kernel that would need room beside the fills
+(link_ipc).  With GA_SLAB_EDGE=bands (and for CPU engines) the
+column is streamed in row bands through the process group instead:
 
 * rank r's fill publishes its right edge row by row into ``halo_out`` and a
   progress word in pinned host memory; the host thread sends each band to
@@ -192,6 +198,28 @@ def _halos(engine, links, m, torch):
     return halo_in, halo_out
 
 
+def edge_mode(engine):
+    """How a slab's edges cross to the next rank: "ipc" -- the left fill stores them into the right rank's
+    GPU memory, mapped through a HIP IPC handle (engines with slab_link_export; the default) -- or "bands"
+    -- halo bands sent by the host over the process group (RCCL / gloo; GA_SLAB_EDGE=bands, CPU engines)."""
+    mode = os.environ.get("GA_SLAB_EDGE", "ipc")
+    if mode not in ("ipc", "bands"):
+        raise ValueError(f"GA_SLAB_EDGE={mode!r}: expected 'ipc' or 'bands'")
+    return mode if hasattr(engine, "slab_link_export") else "bands"
+
+
+def link_ipc(dist, links, engine):
+    """Link this rank's slab to its neighbours for one problem: export its left-edge buffer to rank - 1, map
+    rank + 1's as its right edge.  The exporter zeroes its progress word before sending the handle, and the
+    importer launches its fill only after receiving it, so a fill never writes an edge its reader is still
+    reading from the previous problem (that reader exports only when it starts the next)."""
+    rank, world = links.rank, links.world
+    if rank > 0:
+        _send_obj(dist, engine.slab_link_export(), rank - 1, links.ctrl)
+    if rank < world - 1:
+        engine.slab_link_import(_recv_obj(dist, rank + 1, links.ctrl))
+
+
 def _send_obj(dist, obj, dst, group):
     dist.send_object_list([obj], dst=dst, group=group)
 
@@ -214,18 +242,26 @@ def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_
     edges = slab_bounds(n, world)
     c0, c1 = edges[rank], edges[rank + 1]
     engine.load_slab(a_codes, b_codes, tables, c0, c1)
-    halo_in, halo_out = _halos(engine, links, m, torch)
-    engine.slab_bind_halos(halo_in.data_ptr() if rank > 0 else 0, halo_out.data_ptr() if rank < world - 1 else 0,
-                           halo_in, halo_out)
-    if links.device_tensors:
-        # the halo tensors come from torch's allocator on torch's stream: the fill's stream
-        # starts after whatever that stream still has in flight
-        engine.order_after(torch.cuda.current_stream().cuda_stream)
-    engine.slab_launch(traceback=traceback)
-    if traceback:
-        engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
-    stream_edges(dist, links, engine, halo_in, halo_out, m, band)
-    cost = engine.slab_finish()
+    if edge_mode(engine) == "ipc":
+        # the fills store the edges into their right neighbours' memory themselves
+        link_ipc(dist, links, engine)
+        engine.slab_launch(traceback=traceback)
+        if traceback:
+            engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
+        cost = engine.slab_finish()
+    else:
+        halo_in, halo_out = _halos(engine, links, m, torch)
+        engine.slab_bind_halos(halo_in.data_ptr() if rank > 0 else 0, halo_out.data_ptr() if rank < world - 1 else 0,
+                               halo_in, halo_out)
+        if links.device_tensors:
+            # the halo tensors come from torch's allocator on torch's stream: the fill's stream
+            # starts after whatever that stream still has in flight
+            engine.order_after(torch.cuda.current_stream().cuda_stream)
+        engine.slab_launch(traceback=traceback)
+        if traceback:
+            engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill
+        stream_edges(dist, links, engine, halo_in, halo_out, m, band)
+        cost = engine.slab_finish()
     ctrl = links.ctrl
     if not traceback:
         if world > 1:
@@ -368,6 +404,12 @@ class GpuSlabEngine:
     def slab_link(self, right):
         self.eng.slab_link(right.eng)
 
+    def slab_link_export(self):
+        return self.eng.slab_link_export()
+
+    def slab_link_import(self, handle):
+        self.eng.slab_link_import(handle)
+
     def order_after(self, stream):
         self.eng.wait_stream(stream)
 
@@ -497,7 +539,9 @@ def bench_main(args, wl, workload):
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (SplitMix64, SURVEY 8d)",
-            "config": {"workload": f"{wl['desc']}; {world} column slabs, banded RCCL edge exchange ({band}-row bands)"
+            "config": {"workload": f"{wl['desc']}; {world} column slabs, "
+                                   + ("edges stored by each fill into the next GPU's memory (IPC-mapped, xGMI)"
+                                      if edge_mode(engine) == "ipc" else f"banded RCCL edge exchange ({band}-row bands)")
                                    + ("; right-to-left walk hand-off" if wl["traceback"] else ""),
                        "m": m, "n": n, "traceback": wl["traceback"], "parallelism": f"column slabs x{world}",
                        "backend": dist.get_backend(), "cost": int(cost), "oracle_cost": gold,

@@ -136,6 +136,14 @@ int ga_slab_bind_halos(ga_ctx* ctx, void* halo_in, void* halo_out);
  * Replaces the pinned-host halos + host relay of round 2 (reference: none -- the reference is
  * single-threaded CPU code). */
 int ga_slab_link(ga_ctx* left, ga_ctx* right);
+/* The same link between two PROCESSES (one GPU each, bench.py --gpus N): the right slab's context allocates
+ * its left edge + progress word (uncached, on its GPU; zeroing the word) and exports an IPC handle
+ * (HIP_IPC_HANDLE_SIZE = 64 bytes); the left slab's context maps it (hipIpcOpenMemHandle, peer access
+ * enabled lazily; kept while the handle stays the same) and its fill stores the edge there directly.
+ * Per problem: export on the right, hand the bytes over (any channel), import on the left, and launch
+ * the left fill only after the right side's export returned (the word is zero). */
+int ga_slab_link_export(ga_ctx* right, void* handle_out);
+int ga_slab_link_import(ga_ctx* left, const void* handle);
 /* Let `device` read and write `peer`'s memory (hipDeviceEnablePeerAccess); GA_OK if already enabled. */
 int ga_enable_peer_access(int device, int peer);
 /* Launch the slab fill asynchronously on the context's compute stream. */

@@ -35,17 +35,19 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def _halo_copy(stream, dst, src, rows, blocks=64):
-    """ga_debug_halo_copy: an RCCL-shaped copy kernel (256 threads, 20 KB LDS, > 256 registers per lane)."""
+def _halo_copy(stream, dst, src, rows, variant, blocks=64):
+    """ga_debug_halo_copy: an RCCL-shaped copy kernel.  variant 0: 256 threads, 20 KB LDS, > 256 registers
+    per lane; 1: RCCL 7.2's own gfx950 send/recv kernel resources (512 threads, 37 664 B LDS, 256 VGPRs)."""
     import ctypes as C
     from globalign_amd import _native
     f = _native.load_library().ga_debug_halo_copy
-    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32]
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32]
     f.restype = C.c_int
-    assert f(stream, dst, src, rows, blocks) == 0
+    assert f(stream, dst, src, rows, blocks, variant) == 0
 
 
-def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, traceback=False, heavy=False):
+def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, traceback=False, heavy=None):
+    """heavy: None (the halo lands through a torch elementwise kernel) or a ga_debug_halo_copy variant."""
     """-> dict(cost, all_done_while_waiting, waited_s, fill_still_waiting, priority, kind)."""
     import torch
     from globalign_amd import _native
@@ -75,8 +77,8 @@ def run_coresidency(m=6000, n=4096, split=2048, nstreams=8, deadline_s=10.0, tra
     for k, s in enumerate(streams):
         with torch.cuda.stream(s):
             if k == nstreams // 2:
-                if heavy:
-                    _halo_copy(s.cuda_stream, halo.data_ptr(), edge.data_ptr(), m + 1)
+                if heavy is not None:
+                    _halo_copy(s.cuda_stream, halo.data_ptr(), edge.data_ptr(), m + 1, heavy)
                 else:
                     torch.add(edge, 0, out=halo)  # the halo lands through an elementwise kernel
             x = torch.arange(1 << 16, device=dev, dtype=torch.int32)
@@ -125,20 +127,18 @@ def test_kernel_on_later_stream_runs_beside_waiting_slab_fill(traceback):
     assert r["cost"] == oracle_cost(*r["seqs"])
 
 
-def test_rccl_shaped_kernel_runs_beside_c4_slab_fill(monkeypatch):
-    """The same at the occupancy of a C4 slab at N = 8 (1M x 125k per GPU): a 125 440-column
-    slab in 64 x 2-column lane stripes, 4 compute waves + 1 IO wave per workgroup, 245 workgroups (one per
-    CU on 245 of the 256 CUs), each holding its LDS rings and profile table.  The halo arrives through a
-    kernel shaped like RCCL's receive kernel (256 threads, 20 KB LDS, > 256 registers per lane), which
-    must start and finish while the fill waits.  The cost must equal the one-GPU fill's."""
+@pytest.mark.parametrize("variant", [0, 1])
+def test_rccl_shaped_kernel_runs_beside_c4_slab_fill(variant):
+    """The same at the geometry of a C4 slab at N = 2 (1M rows, 499 712 columns).  The halo
+    arrives through a kernel shaped like RCCL's (variant 0: 256 threads, 20 KB LDS, > 256 registers per
+    lane; 1: RCCL 7.2's own send/recv kernel resources, a CU of its own), which must start and finish while
+    the fill waits.  A slab whose edges a kernel moves keeps one CU of every shader engine free
+    (lane_geometry): here one round of at most 224 workgroups.  The cost must equal the one-GPU fill's."""
     from globalign_amd import _native
-    monkeypatch.setenv("GA_LANE_COLS_PER_LANE", "2")
-    monkeypatch.setenv("GA_FILL_NWC", "4")
-    monkeypatch.setenv("GA_FILL_MODE", "lane")
-    m, split, width = 20_000, 2048, 245 * 4 * 128
-    r = run_coresidency(m=m, n=split + width, split=split, heavy=True, deadline_s=20.0)
+    m, split, width = 1_000_000, 2048, 499_712
+    r = run_coresidency(m=m, n=split + width, split=split, heavy=variant, deadline_s=20.0)
     kind = r["kind"]
-    assert kind[0] == "lane" and kind[1] == 2 and kind[3] == 4 and kind[4] == 245, kind
+    assert kind[0] == "lane" and kind[4] <= 224, kind
     assert r["all_done_while_waiting"], f"the RCCL-shaped kernel did not run beside the waiting fill ({r})"
     assert r["fill_still_waiting"], "the slab fill finished before its halo was released"
     assert r["halo_ok"]

@@ -1,9 +1,11 @@
 """Multi-rank path with the product engine on one MI355X: two ranks on cuda:0 over gloo.
 
-Both ranks' slab fills run concurrently on the same GPU; the left / right
-edges travel through pinned host tensors (the gloo transport), the progress
-words through pinned host memory, exactly as distributed.py drives RCCL on a
-multi-GPU node.  The result must equal the single-problem oracle.
+Both ranks' slab fills run concurrently on the same GPU.  The edges cross either
+through IPC-mapped device memory that each fill stores into itself (edge mode
+"ipc", the default: the cross-process hand-off bench.py --gpus N uses between
+GPUs), or in row bands through pinned host tensors (the gloo transport) with
+progress words in pinned host memory, as distributed.py drives RCCL bands
+(GA_SLAB_EDGE=bands).  The result must equal the single-problem oracle.
 """
 import os
 import random
@@ -62,8 +64,14 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("edge", ["ipc", "bands"])
 @pytest.mark.parametrize("world,m,n,seed,band", [(2, 3000, 5000, 21, 512), (3, 2100, 4100, 8, 700)])
-def test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path):
+def test_gpu_slabs_edge_modes_match_oracle(world, m, n, seed, band, edge, tmp_path, monkeypatch):
+    monkeypatch.setenv("GA_SLAB_EDGE", edge)
+    _slabs_match_oracle(world, m, n, seed, band, tmp_path)
+
+
+def _slabs_match_oracle(world, m, n, seed, band, tmp_path):
     import torch.multiprocessing as mp
     from oracle import core
     seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
@@ -80,8 +88,14 @@ def test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path):
     assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
 
 
+@pytest.mark.parametrize("edge", ["ipc", "bands"])
 @pytest.mark.parametrize("world,m,n,seed,band", [(2, 4000, 60_000, 41, 1024), (3, 3000, 40_000, 43, 600)])
-def test_gpu_slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
+def test_gpu_slabs_score_only_edge_modes_match_oracle(world, m, n, seed, band, edge, tmp_path, monkeypatch):
+    monkeypatch.setenv("GA_SLAB_EDGE", edge)
+    _slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path)
+
+
+def _slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
     """Strong-scaling bench path (C4 shape): score only, each rank's slab many workgroup slabs (60k columns
     over 2 ranks = 2 x 118 workgroups).  The ranks share one GPU here, so all their workgroups must be
     co-resident (<= 256 CUs; each rank's first slab waits on the other rank).  Cost vs the C oracle."""
@@ -109,8 +123,8 @@ def test_gpu_slabs_score_only_diag_match_oracle(td, monkeypatch, tmp_path):
     edge from the neighbour rank's progress word, the right edge out to it, the cost from the last rank."""
     monkeypatch.setenv("GA_FILL_MODE", "diag")
     monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
-    test_gpu_slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
-    test_gpu_slabs_score_only_match_oracle(3, 12_000, 2_000 + 5, 47 + td, 2048, tmp_path)
+    _slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
+    _slabs_score_only_match_oracle(3, 12_000, 2_000 + 5, 47 + td, 2048, tmp_path)
 
 
 @pytest.mark.parametrize("devices,m,n,seed,kw", [
@@ -145,7 +159,7 @@ def test_gpu_slabs_recompute_walk_match_oracle(world, m, n, seed, band, tmp_path
     handed on right to left, recomputes the blocks ahead of it -- the leftmost slabs' stripe 0 from the
     halo the left neighbour sent."""
     monkeypatch.setenv("GA_RC", "1")
-    test_gpu_slabs_match_oracle(world, m, n, seed, band, tmp_path)
+    _slabs_match_oracle(world, m, n, seed, band, tmp_path)
 
 
 def test_global_aligner_devices_recompute_walk(monkeypatch):
