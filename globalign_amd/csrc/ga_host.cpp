@@ -738,7 +738,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // one round of lane workgroups (every stripe resident): the chain's lag counts, read edges late
     p.late = c->lane && c->nslabs <= c->num_cu ? 1 : 0;
     if (const char* e = getenv("GA_LANE_LATE")) p.late = atoi(e);
-    p.hand_direct = 1;
+    p.hand_direct = 0;  // measured: C4 210 ms against 221 with the direct hand-off, 1M x 125k 52.5 against 56 (r3_c4.log)
     if (const char* e = getenv("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
     p.stck_every = bd.rc_every;
     if (bd.rc) {

@@ -38,7 +38,8 @@ for cfg in servers:
         L.ga_debug_walk(eng._h, w.ctypes.data)
         rc = np.zeros(4, dtype=np.uint32)
         L.ga_debug_rc(eng._h, rc.ctypes.data)
-        print(f"servers={ns} win={win} wpw={wpw} fill={t['fill_ms']:.3f} walk={t['walk_ms']:.3f} call={t['call_ms']:.3f} kind={eng.fill_kind()} "
+        steps = len(r[1][0])
+        print(f"steps={steps} ns_per_step={t['walk_ms'] * 1e6 / steps:.1f} servers={ns} win={win} wpw={wpw} fill={t['fill_ms']:.3f} walk={t['walk_ms']:.3f} call={t['call_ms']:.3f} kind={eng.fill_kind()} "
               f"walk: waits={w[0]} tiles={w[1]} t_tile_ms={w[2] / 1e5:.3f} t_ring_ms={w[3] / 1e5:.3f} t_total_ms={w[4] / 1e5:.3f} "
               f"loads={w[7]} load_us_avg={w[6] / max(w[7], 1) / 100:.2f} | rc blocks={rc[2]} block_us_avg={rc[3] / max(rc[2], 1) / 100:.2f}",
               flush=True)
