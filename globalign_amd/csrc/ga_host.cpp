@@ -1133,7 +1133,9 @@ bool rc_eligible(ga_ctx* c) {
     if (mode == 0 || c->slab || c->qbytes != 1 || c->K > 32) return false;
     if (c->m < 256 || c->n < 256) return false;  // (degenerate walks read cells no block ever recomputes)
     if (mode == 1) return true;
-    int64_t min_cells = (int64_t)1 << 27;
+    // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
+    // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
+    int64_t min_cells = (int64_t)1 << 32;
     if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
     return c->m * c->n >= min_cells;
 }
@@ -1249,7 +1251,9 @@ bool rc_slab_eligible(ga_ctx* c) {
     const int mode = e ? atoi(e) : -1;
     if (mode == 0 || c->qbytes != 1 || c->K > 32 || c->m < 256 || c->n < 256) return false;
     if (mode == 1) return true;
-    int64_t min_cells = (int64_t)1 << 27;
+    // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
+    // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
+    int64_t min_cells = (int64_t)1 << 32;
     if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
     return c->m * c->n >= min_cells;
 }
@@ -1685,10 +1689,13 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // the walks chained in one launch (align_chain) behind row-scan fills: C2 0.908 -> 0.823 ms per
         // alignment, C5 1.522 -> 1.507.  Not behind the lane fills: C3 8.96-9.05 -> 9.47-9.55, its four
         // narrow fills (392 workgroups for 256 CUs) running 27.4 -> 29.5 ms each beside a walk that never
-        // gives its CU back (tools/exp/chain_ab.sh).  GA_PIPE_CHAIN=1 / 0 forces it on / off.
+        // gives its CU back (tools/exp/chain_ab.sh).  Opt-in (GA_PIPE_CHAIN=1): the persistent chain polls
+        // host-written words, so a device-synchronising call another thread of the process makes while it
+        // runs (hipFree, hipDeviceSynchronize, a torch allocator release) would wait on it until its 60 s
+        // bound; per-launch walks have no such hazard and cost C2 / C5 ~1-10 % more per alignment.
         const char* ch = getenv("GA_PIPE_CHAIN");
         const bool fits = (int64_t)count * (c->m + c->n + 1) <= ((int64_t)256 << 20);  // 1 GB of entries
-        const bool on = ch ? atoi(ch) != 0 : c->pipe_lane_td == 0;
+        const bool on = ch != nullptr && atoi(ch) != 0;
         if (on && fits && c->walk_cus == 0 && !getenv("GA_PIPE_FILL_PRIO") && !getenv("GA_PIPE_ROW_FIRST"))
             return align_chain(c, count, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out, t0);
     }

@@ -116,7 +116,7 @@ def test_align_repeated_pipe_modes(monkeypatch, mode, fills, m, n, seed, count, 
     (40000, 300, 15, 7, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)),
 ])
 def test_align_repeated_walk_chain(monkeypatch, chain, m, n, seed, count, kw):
-    """Walks chained in one launch (walk_chain_kernel, the default) and one launch per walk (GA_PIPE_CHAIN=0):
+    """Walks chained in one launch (walk_chain_kernel, opt-in GA_PIPE_CHAIN=1) and one launch per walk (the default):
     more alignments than slots (every slot reused), short walks that outrun the tie-break producer, a tall
     pair; each alignment's strings and cost and the final random state equal the chained oracle's."""
     import globalign_amd

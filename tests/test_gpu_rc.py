@@ -2,7 +2,7 @@
 stripe's right edge, staircase lane states every GA_RC_EVERY steps), then one launch in which workgroup 0
 walks while recompute workgroups rebuild the traceback words of the 64-row blocks ahead of it.  The result
 must equal the single-problem oracle exactly: cost, the three alignment strings, the final random state.
-GA_RC=1 forces the path at small sizes; the full-size C3 / C5 pins take it by default
+GA_RC=1 forces the path at small sizes; the full-size C3 pin takes it by default
 (test_gpu_parity.py::test_bench_workload_cost_matches_golden)."""
 import random
 

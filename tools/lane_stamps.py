@@ -20,8 +20,14 @@ from globalign_amd import _native  # noqa: E402
 
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 125_000
-s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
-tables, _ = bench.problem_tables(s1, s2)
+# optional third argument: a bench workload whose alphabet, seeds and scoring to use (e.g. c5)
+wl = bench.WORKLOADS[sys.argv[3]] if len(sys.argv) > 3 else None
+if wl:
+    s1, s2 = bench.splitmix(m, wl["seeds"][0], wl["alphabet"]), bench.splitmix(n, wl["seeds"][1], wl["alphabet"])
+    tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
+else:
+    s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
+    tables, _ = bench.problem_tables(s1, s2)
 eng = _native.Engine(0)
 eng.load(tables.codes(s1), tables.codes(s2), tables)
 L = _native.load_library()
