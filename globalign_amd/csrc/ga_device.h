@@ -79,6 +79,10 @@ struct WalkArgs {
     unsigned rc_ready;
     int rc_nbs, rc_td;         // blocks per block row; 64-column tiles per block (the fill's TD)
     unsigned* rc_pos;          // [0] the walker's tile (ti << 16 | tj), [1] 1 once the walk has ended
+    // optional (nullptr): dispatches whose levels are in `ops` (pinned host memory then), raised by the
+    // helper after each flush with a system-scope release, the exact count once the walk has ended -- the
+    // host decodes the alignment while the walk runs (rc_align)
+    unsigned* ops_prog;
 };
 
 // The recompute walk's tile cache: block (bi, bs) (64 rows of fill stripe bs) lives at slot

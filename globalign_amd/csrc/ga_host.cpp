@@ -393,6 +393,10 @@ struct ga_ctx {
     char peer_handle[64] = {};
     unsigned rc_epoch = 0;
     bool rc_used = false;  // the last fill was the recompute path's (ga_problem_align or a slab's)
+    // rc_align's walk levels in pinned host memory and the helper's progress word: decoded while the walk runs
+    uint32_t* rc_ops_pin = nullptr;
+    int64_t rc_ops_cap = 0;  // words
+    unsigned* rc_ops_prog = nullptr;
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
     int rc_every_used = 64;
 };
@@ -857,6 +861,7 @@ struct WalkBufs {
     hipEvent_t ev0, ev1;
     const int* bnd_row = nullptr;  // the boundary triples (nullptr: the context's)
     const int* bnd_col = nullptr;
+    unsigned* ops_prog = nullptr;  // WalkArgs::ops_prog (ops then in pinned host memory)
 };
 WalkBufs ctx_walk_bufs(ga_ctx* c) {
     return WalkBufs{c->tb.as<uint8_t>(), c->rng.as<uint32_t>(), c->ops.as<uint32_t>(), c->result.as<int>(), c->stream,
@@ -900,6 +905,7 @@ ga::WalkArgs walk_args(ga_ctx* c, int64_t ntab, const WalkStart& st, int64_t r0,
         w.nloaders = nl ? atoi(nl) : 14;
     }
     w.ops = wb.ops;
+    w.ops_prog = wb.ops_prog;
     w.result = wb.result;
     w.dbg = nullptr;
     return w;
@@ -1271,14 +1277,120 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     WalkBufs wb = ctx_walk_bufs(c);
     const int64_t ntab = (int64_t)R.tab.size();
     HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    // the walk's levels go to pinned host memory, and this thread decodes them while the walk runs
+    const int64_t nwords = (m + n + 1 + 15) / 16 + 64;
+    if (c->rc_ops_cap < nwords) {
+        if (c->rc_ops_pin) HIPCHK(hipHostFree(c->rc_ops_pin));
+        c->rc_ops_pin = nullptr;
+        c->rc_ops_cap = 0;
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, sizeof(uint32_t) * nwords, hipHostMallocMapped | hipHostMallocCoherent));
+        c->rc_ops_pin = static_cast<uint32_t*>(hp);
+        c->rc_ops_cap = nwords;
+    }
+    if (!c->rc_ops_prog) {
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        c->rc_ops_prog = static_cast<unsigned*>(hp);
+    }
+    __atomic_store_n(c->rc_ops_prog, 0u, __ATOMIC_SEQ_CST);
+    {
+        void* dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, c->rc_ops_pin, 0));
+        wb.ops = static_cast<uint32_t*>(dp);
+        HIPCHK(hipHostGetDevicePointer(&dp, c->rc_ops_prog, 0));
+        wb.ops_prog = static_cast<unsigned*>(dp);
+    }
     const WalkStart st0{m, n, 0, 0, 0, 1};
     if (int r = rc_walk_launch(c, ntab, st0, wb)) return r;
-    if (int rr = finish_fill(c, cost_out, nullptr)) return rr;
     WalkStart st = st0;
     int reason = 0;
     int64_t len = 0;
-    if (int rr = walk_segment(c, st, reason, a_chr, b_chr, oa, om, ob, cap, len, &wb)) return rr;
-    if (reason == 7) return fail(GA_E_TIMEOUT, "recompute walk: a tile was never recomputed");
+    {
+        // decode dispatches [D, D1) of the levels (dp_array_backward's column output, in walk order)
+        const uint32_t* ops = c->rc_ops_pin;
+        int64_t i = st.i, j = st.j, D = st.D;
+        int L = st.L;
+        auto decode_to = [&](int64_t D1) {
+            for (; D < D1; D++) {
+                const char ca = a_chr[pywrap(i - 1, m)], cbb = b_chr[pywrap(j - 1, n)];
+                const unsigned lv = (ops[D >> 4] >> (30 - 2 * (D & 15))) & 3u;
+                const int64_t k = len++;
+                if (k < cap) {
+                    if (lv == 0) { oa[k] = ca; om[k] = ca == cbb ? '|' : '*'; ob[k] = cbb; }
+                    else if (lv == 1) { oa[k] = '-'; om[k] = ' '; ob[k] = cbb; }
+                    else { oa[k] = ca; om[k] = ' '; ob[k] = '-'; }
+                }
+                i -= lv != 1;
+                j -= lv != 2;
+                L = (int)lv;
+            }
+        };
+        static const int64_t lag = [] {
+            const char* e = getenv("GA_RC_DECODE_LAG");  // (diagnostics) blocks of 512 dispatches held back
+            return e ? (int64_t)atoi(e) * 512 : (int64_t)0;
+        }();
+        std::vector<uint32_t> seen;  // (diagnostics) GA_RC_DECODE_CHECK: the words as decoded
+        const bool check = getenv("GA_RC_DECODE_CHECK") != nullptr;
+        if (check) seen.assign((size_t)nwords, 0u);
+        for (;;) {
+            const unsigned pr = __atomic_load_n(c->rc_ops_prog, __ATOMIC_ACQUIRE);
+            if ((int64_t)pr - lag > D) {
+                if (check)
+                    for (int64_t q = D >> 4; q < (((int64_t)pr - lag + 15) >> 4); q++) seen[q] = ops[q];
+                decode_to((int64_t)pr - lag);
+                continue;
+            }
+            const hipError_t q = hipStreamQuery(wb.stream);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return fail(GA_E_HIP, std::string("walk: ") + hipGetErrorString(q));
+            std::this_thread::yield();
+        }
+        // the fill ran before the walk on the same stream: its cost (and any abort) now, with no wait
+        if (int rr = finish_fill(c, cost_out, nullptr)) return rr;
+        int res[16];
+        HIPCHK(hipMemcpy(res, wb.result, sizeof(res), hipMemcpyDeviceToHost));
+        HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
+        c->walk_waits = res[4];
+        c->walk_tiles = res[5];
+        c->walk_t_tile = res[6];
+        c->walk_t_ring = res[7];
+        c->walk_t_total = res[8];
+        c->walk_c_total = res[9];
+        c->walk_load_ticks = res[10];
+        c->walk_load_count = res[11];
+        reason = res[3];
+        if (reason == 7) return fail(GA_E_TIMEOUT, "recompute walk: a tile was never recomputed");
+        const int64_t D1 = res[0];
+        if (D > D1) return fail(GA_E_STATE, "walk levels published past the walk's end");
+        if (check) {
+            int64_t bad = 0, first_bad = -1;
+            for (int64_t q = 0; q < (D >> 4); q++)
+                if (seen[q] != ops[q]) {
+                    bad++;
+                    if (first_bad < 0) first_bad = q;
+                }
+            if (bad)
+                return fail(GA_E_STATE, "decode check: " + std::to_string(bad) + " level words changed after decode, first " +
+                                            std::to_string(first_bad) + " of " + std::to_string(D >> 4) + " (D1 " +
+                                            std::to_string(D1) + ")");
+        }
+        decode_to(D1);
+        if (reason == 4) {  // (never here: such walks are degenerate, reason 7) the reference's IndexError
+            len = 0;
+            i = st.i;
+            j = st.j;
+        }
+        if (D1 > st.D) {
+            st.h += (D1 - st.D) - (st.first ? 1 : 0);
+            st.first = 0;
+        }
+        st.i = i;
+        st.j = j;
+        st.L = L;
+        st.D = D1;
+        if (len > cap) return fail(GA_E_ARG, "output capacity too small");
+    }
     const int rc = conclude_walk(R, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
     return rc;
@@ -2007,6 +2119,8 @@ void ga_ctx_destroy(ga_ctx* c) {
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     if (c->peer_link) (void)hipIpcCloseMemHandle(c->peer_link);
+    if (c->rc_ops_pin) (void)hipHostFree(c->rc_ops_pin);
+    if (c->rc_ops_prog) (void)hipHostFree(c->rc_ops_prog);
     for (auto& sl : c->pipe) {
         for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result, &sl.GVp, &sl.GHp,
                           &sl.top, &sl.left, &sl.bnd_row, &sl.bnd_col, &sl.meta, &sl.bscr})

@@ -323,8 +323,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         long long rl = w.D0 >> 9, fl = w.D0 >> 9;
         int pub = -1;  // RC: the walker's tile last published for the recompute workgroups
         for (;;) {
-            const int d = sgpr(__hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS));
+            // done first: the walker stores its final dispatch count before walk_done, so once done is seen
+            // d is final (read the other way round, a stale d beside done = 1 dropped the last levels)
             const int done = sgpr(__hip_atomic_load(&walk_done, __ATOMIC_ACQUIRE, WGS));
+            const int d = sgpr(__hip_atomic_load(&wD, __ATOMIC_ACQUIRE, WGS));
             bool moved = false;
             if constexpr (RC) {
                 const int cur = sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_ACQUIRE, WGS));
@@ -343,11 +345,26 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                 moved = true;
             }
             const long long complete = done ? ((long long)d + 511) / 512 : (d >> 9);
+            const long long fl0 = fl;
             while (fl < complete) {  // 512 dispatches = 32 words of levels
-                if (lane < 32) w.ops[fl * 32 + lane] = opsbuf[(fl & 3) * 32 + lane];
+                if (lane < 32) {
+                    const uint32_t v = opsbuf[(fl & 3) * 32 + lane];
+                    // host-polled levels (ops_prog): write-through system-scope stores, like a halo's rows
+                    if (w.ops_prog != nullptr) __hip_atomic_store(w.ops + fl * 32 + lane, v, RLX, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else w.ops[fl * 32 + lane] = v;
+                }
                 fl++;
                 if (lane == 0) __hip_atomic_store(&ops_flushed, (int)fl, __ATOMIC_RELEASE, WGS);
                 moved = true;
+            }
+            if (w.ops_prog != nullptr && fl > fl0) {
+                // the host's decode may run up to here: whole blocks while walking, every dispatch at the end.
+                // The level stores complete first (a release fence alone left a block stale on the host: its
+                // L2 write-back was not awaited before the progress store, tools/exp/r3_dec.sh)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(w.ops_prog, done ? (unsigned)d : (unsigned)(fl * 512), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
             }
             if (done && fl >= complete) break;
             if (!moved) __builtin_amdgcn_s_sleep(RC ? 2 : 8);
@@ -714,6 +731,7 @@ __device__ __forceinline__ WalkArgs uniform_walk_args(const WalkArgs& s) {
     w.nloaders = sgpr(s.nloaders);
     w.rc_flags = nullptr;
     w.rc_pos = nullptr;
+    w.ops_prog = nullptr;
     return w;
 }
 
