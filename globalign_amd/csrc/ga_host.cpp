@@ -1190,7 +1190,10 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     wb.tb = c->rc_tb.as<uint8_t>();
     ga::WalkArgs w = walk_args(c, ntab, st, 0, -1, false, wb);
     w.TC = ga::RC_CACHE * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
-    w.nloaders = 14;                // no L2 prefetcher (it would read blocks not yet recomputed)
+    // 14 loaders, no L2 prefetcher (it would read blocks not yet recomputed); GA_RC_LOADERS = 12 / 13 leave
+    // waves 8 and 12 / wave 8 (the walker's SIMD) idle instead
+    w.nloaders = 14;
+    if (const char* e = getenv("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
     w.rc_flags = c->rc_flags.as<unsigned>();
     w.rc_ready = 2u * c->rc_epoch + 1u;
     w.rc_nbs = nbs;

@@ -288,6 +288,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
     // loader waves (WalkArgs::nloaders): 12, or 13 with wave 12, or 14 with wave 8 too (no prefetcher)
     const int nload = w.nloaders >= 12 && w.nloaders <= NLOAD_MAX ? w.nloaders : 12;
     const bool prefetch = nload < 14, idle12 = nload < 13;
+    if (RC && wave == 8 && prefetch) return;  // the recompute walk's words may not be written yet: no prefetch
     if (wave == 8 && prefetch) {
         // ---------------- L2 prefetcher: touches the ring of tiles just beyond the loaders'
         // 4x4 block (offsets with i+j distance 4..6, each <= 4), so their HBM fetch is
