@@ -555,7 +555,7 @@ def bench_main(args, wl, workload):
             "roofline": dict(bench.roofline(workload, dict(wl, n=max(b - a for a, b in zip(edges, edges[1:]))),
                                             fill_max, profile_cells=m * n),
                              note="per-cell SQ_INSTS_VALU / PMC bytes of the 1-GPU profile scaled to the widest slab; "
-                                  "slab fill time includes the wait for the left neighbour's first band")
+                                  "slab fill time includes the wait for the left neighbour's first rows")
             if fill_max > 0 else None,
         }
         print(json.dumps(line), flush=True)
