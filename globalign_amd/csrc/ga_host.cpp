@@ -2282,6 +2282,8 @@ int ga_slab_bind_halos(ga_ctx* c, void* halo_in, void* halo_out) {
     if (!c->slab) return fail(GA_E_STATE, "not a slab context");
     c->halo_in_ext = static_cast<int2*>(halo_in);
     c->halo_out_ext = static_cast<int2*>(halo_out);
+    // bound halos go with the context's own (host-relayed) progress words, not a link's
+    c->in_prog_ext = c->out_prog_ext = nullptr;
     return GA_OK;
 }
 

@@ -86,6 +86,8 @@ class Links:
         backend = dist.get_backend()
         self.ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
         self.device_tensors = backend != "gloo"
+        self.ipc_ok = None  # edge links through IPC: agreed by every rank on the first problem (ipc_agreed)
+        self.ipc_linked_now = False
 
     def warm_up(self, dist, torch, device):
         """Create the pair communicators now (one tiny exchange each way on every pair group).
@@ -208,6 +210,26 @@ def edge_mode(engine):
     return mode if hasattr(engine, "slab_link_export") else "bands"
 
 
+def ipc_agreed(dist, links, engine):
+    """Whether every rank could link its edges through IPC, decided once per process group (the first
+    problem): each rank links (`link_ipc`) and reports; if any failed -- a handle that does not open, no
+    peer path between two GPUs -- every rank uses bands from then on.  Collective over all ranks."""
+    if links.ipc_ok is None:
+        import torch
+        ok = 1
+        try:
+            link_ipc(dist, links, engine)
+        except Exception as e:  # noqa: BLE001 (any failure to link falls back, reported on stderr)
+            import sys
+            print(f"rank {links.rank}: IPC edge link failed ({e}); using bands", file=sys.stderr, flush=True)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=links.ctrl)
+        links.ipc_ok = bool(int(flag[0]))
+        links.ipc_linked_now = links.ipc_ok  # this problem is already linked
+    return links.ipc_ok
+
+
 def link_ipc(dist, links, engine):
     """Link this rank's slab to its neighbours for one problem: export its left-edge buffer to rank - 1, map
     rank + 1's as its right edge.  The exporter zeroes its progress word before sending the handle, and the
@@ -242,9 +264,12 @@ def align_slabs(dist, links, engine, seq_1, seq_2, a_codes, b_codes, tables, mt_
     edges = slab_bounds(n, world)
     c0, c1 = edges[rank], edges[rank + 1]
     engine.load_slab(a_codes, b_codes, tables, c0, c1)
-    if edge_mode(engine) == "ipc":
+    if edge_mode(engine) == "ipc" and ipc_agreed(dist, links, engine):
         # the fills store the edges into their right neighbours' memory themselves
-        link_ipc(dist, links, engine)
+        if links.ipc_linked_now:
+            links.ipc_linked_now = False
+        else:
+            link_ipc(dist, links, engine)
         engine.slab_launch(traceback=traceback)
         if traceback:
             engine.slab_walk_prepare(mt_words)  # host tie-break table, overlapped with the fill

@@ -125,7 +125,8 @@ int ga_problem_set_slab(ga_ctx* ctx, const uint8_t* a, int64_t m, const uint8_t*
 int ga_slab_buffers(ga_ctx* ctx, void** halo_in, uint32_t** halo_in_prog, void** halo_out, uint32_t** halo_out_prog);
 /* Use caller-owned device buffers ((m+1) x int2 each) as the slab's left-edge
  * input and right-edge output (e.g. tensors that RCCL receives into / sends
- * from); NULL keeps the context's own buffer. */
+ * from); NULL keeps the context's own buffer.  Their progress goes through the context's own
+ * words (ga_slab_buffers): this undoes a ga_slab_link / _export / _import. */
 int ga_slab_bind_halos(ga_ctx* ctx, void* halo_in, void* halo_out);
 /* Join two neighbouring slab contexts of ONE process (GlobalAligner(devices=[...])) device to device: the
  * right context allocates its left edge (m + 1 int2 rows) and a progress word in uncached device memory

@@ -35,7 +35,7 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True):
+def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True, fail_import=False):
     import torch
     import torch.distributed as dist
     from globalign_amd import distributed
@@ -48,10 +48,16 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback
         tables = CostTables(cmat, goc)
         links = distributed.Links(dist, rank, world)
         eng = distributed.GpuSlabEngine(0)
+        if fail_import and rank == 0:
+            def refuse(handle):
+                raise RuntimeError("simulated: the right neighbour's IPC handle does not open")
+            eng.slab_link_import = refuse
         for _ in range(2):  # the second run reuses the context (buffers, progress words)
             res = distributed.align_slabs(dist, links, eng, seq_1, seq_2, tables.codes(seq_1),
                                           tables.codes(seq_2), tables, mt_words, band=band, torch=torch,
                                           traceback=traceback)
+        if fail_import:
+            assert links.ipc_ok is False  # every rank fell back to bands
         if rank == 0:
             cost, strings, status, mt_after = res
             if traceback:
@@ -214,3 +220,23 @@ def test_linked_slabs_abort_propagates(monkeypatch):
     finally:
         for eng in engines:
             eng.eng.close()
+
+
+def test_gpu_slabs_ipc_failure_falls_back_to_bands(tmp_path):
+    """If any rank cannot link its edges through IPC (here rank 0's import is made to fail), every rank agrees
+    on the first problem to use bands instead, and the results stay exact."""
+    import torch.multiprocessing as mp
+    from oracle import core
+    m, n, seed, world = 2500, 4600, 71, 3
+    seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
+    random.seed(seed)
+    mt_words = np.array(random.getstate()[1], dtype=np.uint32)
+    out = str(tmp_path / "res_fb.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, 600, out, True, True), nprocs=world,
+                       join=True, start_method="spawn")
+    r = np.load(out)
+    cmat, goc = _scoring(seq_1, seq_2)
+    ref = core.align(seq_1, seq_2, cmat, goc, mt_words)
+    assert int(r["cost"]) == ref["cost"]
+    assert (str(r["a"]), str(r["mid"]), str(r["b"])) == tuple(ref["strings"])
+    assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
