@@ -609,7 +609,7 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     HIPCHK(c->out_last.ensure(sizeof(int) * 4));
     HIPCHK(c->result.ensure(sizeof(int) * 16));
     HIPCHK(c->ops.ensure(m + n_all + 1024));  // 2-bit levels; the walk flushes whole 128-byte blocks
-    HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2)));
+    HIPCHK(c->rng.ensure(sizeof(uint32_t) * (m + n_all + 2 + 64)));  // + the walk's entry look-ahead (SLD)
     HIPCHK(hipStreamSynchronize(c->stream));
     c->loaded = true;
     c->filled_tb = false;
@@ -1447,7 +1447,7 @@ int pipe_setup(ga_ctx* c) {
             sl.tab_pin = static_cast<uint32_t*>(hp);
             sl.tab_cap = per;
         }
-        HIPCHK(sl.rng.ensure(sizeof(uint32_t) * per));
+        HIPCHK(sl.rng.ensure(sizeof(uint32_t) * (per + 64)));  // + the walk's entry look-ahead (SLD)
         HIPCHK(sl.ops.ensure(c->m + c->n + 1024));
         HIPCHK(sl.result.ensure(sizeof(int) * 16));
         const int64_t m = c->m, na = c->n_global;

@@ -242,7 +242,10 @@ __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
 // torus: TP x TP u16 of LDS (the kernel's).  RC: the recompute walk (ga_rcwalk.hip): a tile
 // is loaded only once its block's flag says another workgroup has written its words (sc1 loads), the
 // helper publishes the walker's tile for those workgroups, and every tile wait is bounded.
-template <int CB, bool RC = false>
+// SLD: the interior walk reads its tie-break entries with scalar loads straight from rng (device memory),
+// a group ahead, instead of from the helper's LDS ring (one ds_read and four readfirstlanes per group);
+// walk_chain_kernel's entries are in pinned host memory and keep the ring
+template <int CB, bool RC = false, bool SLD = true>
 __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng, uint16_t* torus) {
     // the thread index through an opaque copy: in walk_chain_kernel nothing derived from it is hoisted
     // out of the loop over walks (it would stay live in VGPRs across every role's code)
@@ -584,7 +587,19 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             const unsigned u = (unsigned)raw;
             return (int)((u & 31u) | ((u & 0x3e0u) << 3) | ((u & 0x7c00u) << 6));
         };
-        auto tabs = [&](int d) { return *reinterpret_cast<const uint4*>(rngbuf + (d & (RB - 1))); };
+        typedef __attribute__((address_space(4))) const uint32_t const_u32;  // scalar (constant) loads
+        const unsigned long long rng_u = (unsigned long long)rng;
+        const const_u32* rng_s = (const const_u32*)(((unsigned long long)(unsigned)sgpr((int)(rng_u >> 32)) << 32) |
+                                                    (unsigned)sgpr((int)rng_u));
+        auto tabs = [&](int d) -> uint4 {
+            if constexpr (SLD) {
+                const const_u32* p = rng_s + d;
+                asm volatile("" : "+s"(p));  // the address in SGPRs (no vector induction variable)
+                return make_uint4(p[0], p[1], p[2], p[3]);
+            } else {
+                return *reinterpret_cast<const uint4*>(rngbuf + (d & (RB - 1)));
+            }
+        };
 
         if ((D & 511) == 0) {
             block_start(D);
@@ -604,6 +619,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             constexpr bool CHECK = decltype(check_tag)::value;
             const int wcur = wcw;
             const uint4 tc = tnext;
+            // SLD: wait for this group's entries (loaded a group ago) before the new LDS / scalar loads go
+            // out, so that the wait does not also cover them
+            if constexpr (SLD) asm volatile("" ::"s"(tc.x), "s"(tc.y), "s"(tc.z), "s"(tc.w));
             wnext = window(i, j);
             tnext = tabs(gd + 4);
             __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
@@ -644,7 +662,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         for (;;) {
             // iteration of 16 dispatches D .. D+15 (D % 16 == 0)
             if ((D & 511) == 0) block_start(D);
-            if (((D + 16) & 511) == 0) rng_ready(D + 16);
+            if (!SLD && ((D + 16) & 511) == 0) rng_ready(D + 16);
             // every window of this iteration is anchored within 12 steps: rows >= i - 19
             if (__builtin_expect(i - 19 < vlo_i || j - 19 < vlo_j, 0)) verify(i, j);
             if (__builtin_expect(min(i, j) > 16, 1)) {
@@ -777,7 +795,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_chain_kernel(WalkChainAr
         if (!sgpr(go)) return;  // uniform: the walks' control flow and arguments stay scalar
         __threadfence();  // acquire: the slot's traceback words and boundary, written by fill k
         const WalkArgs w = uniform_walk_args(a.w[k % a.S]);
-        walk_body<CB>(w, a.tab + G, torus);
+        walk_body<CB, false, false>(w, a.tab + G, torus);
         if (threadIdx.x == 0) {  // result[12..14]: this walk's wait before it started (ticks, polls)
             w.result[12] = (int)t_wait;
             w.result[13] = wait_fill;
