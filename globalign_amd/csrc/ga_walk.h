@@ -591,10 +591,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         const unsigned long long rng_u = (unsigned long long)rng;
         const const_u32* rng_s = (const const_u32*)(((unsigned long long)(unsigned)sgpr((int)(rng_u >> 32)) << 32) |
                                                     (unsigned)sgpr((int)rng_u));
+        const const_u32* rng_it = rng_s;  // SLD: entries of the current iteration (D .. D+15) and beyond
+        int d_it = 0;
         auto tabs = [&](int d) -> uint4 {
             if constexpr (SLD) {
-                const const_u32* p = rng_s + d;
-                asm volatile("" : "+s"(p));  // the address in SGPRs (no vector induction variable)
+                const const_u32* p = rng_it + (d - d_it);  // a constant offset within an iteration
                 return make_uint4(p[0], p[1], p[2], p[3]);
             } else {
                 return *reinterpret_cast<const uint4*>(rngbuf + (d & (RB - 1)));
@@ -640,7 +641,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                 // the chosen level comes out as the next field's bit offset (lvl * 8): two dependent
                 // scalar ops fewer per step than extracting lvl and scaling it
                 L8 = (t[k] >> ((v >> L8) & 31u)) & 0x18u;
-                A = A * 4u + L8;
+                // A = A * 4 + L8 as the single fused op (the compiler's reassociated form took 11 ops a group)
+                asm volatile("s_lshl2_add_u32 %0, %0, %1" : "+s"(A) : "s"(L8));
                 ix += 0x080109u >> L8;
                 if (CHECK) {
                     const unsigned mv = (ix - rel) & 0xffu;
@@ -657,10 +659,18 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             i -= (int)(mv >> 3);
             j -= (int)(mv & 7u);
             rel = mv;
+            // the widening above stays in this group (scheduled past the boundary it put six VALU ahead of
+            // the next group's first readlane)
+            __builtin_amdgcn_sched_barrier(0);
             return 0;
         };
         for (;;) {
             // iteration of 16 dispatches D .. D+15 (D % 16 == 0)
+            if constexpr (SLD) {
+                rng_it = rng_s + D;
+                asm volatile("" : "+s"(rng_it));  // the address in SGPRs (no vector induction variable)
+                d_it = D;
+            }
             if ((D & 511) == 0) block_start(D);
             if (!SLD && ((D + 16) & 511) == 0) rng_ready(D + 16);
             // every window of this iteration is anchored within 12 steps: rows >= i - 19
