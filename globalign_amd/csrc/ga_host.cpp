@@ -1245,7 +1245,10 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         r.nwin = 48;
         if (const char* e = getenv("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
     }
-    int nserv = 96;
+    // recompute workgroups: with a faster walker (scalar entry loads) fewer workers keep up, and more of them
+    // slow the walker's own tile loads (C3 walk 5.78 / 5.84 / 5.99 / 6.24 ms at 48 / 64 / 96 / 128 workers,
+    // 6.05 at 40, 6.72 at 32: tools/exp/r3b_servers.sh); 64 keeps a margin above the cliff
+    int nserv = 64;
     if (const char* e = getenv("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
     HIPCHK(hipEventRecord(wb.ev0, wb.stream));
     ga::launch_walk_rc(wb.stream, w, r, nserv);
