@@ -1270,20 +1270,10 @@ bool rc_slab_eligible(ga_ctx* c) {
     return c->m * c->n >= min_cells;
 }
 
-int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
-             int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
-    const double t0 = now_ms();
+// One alignment's walk writing its levels to pinned host memory with a progress word (WalkArgs::ops_prog),
+// so that the calling thread decodes them while the walk runs (rc_align, and the stored-words call)
+int pinned_walk_levels(ga_ctx* c, WalkBufs& wb) {
     const int64_t m = c->m, n = c->n;
-    if (int r = rc_fill(c)) return r;
-    // the tie-break table on the host while the device fills
-    RngTable R;
-    const double t1 = now_ms();
-    build_rng(mt_state, m + n + 1, R);
-    c->rng_ms = (float)(now_ms() - t1);
-    WalkBufs wb = ctx_walk_bufs(c);
-    const int64_t ntab = (int64_t)R.tab.size();
-    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
-    // the walk's levels go to pinned host memory, and this thread decodes them while the walk runs
     const int64_t nwords = (m + n + 1 + 15) / 16 + 64;
     if (c->rc_ops_cap < nwords) {
         if (c->rc_ops_pin) HIPCHK(hipHostFree(c->rc_ops_pin));
@@ -1307,8 +1297,17 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
         HIPCHK(hipHostGetDevicePointer(&dp, c->rc_ops_prog, 0));
         wb.ops_prog = static_cast<unsigned*>(dp);
     }
-    const WalkStart st0{m, n, 0, 0, 0, 1};
-    if (int r = rc_walk_launch(c, ntab, st0, wb)) return r;
+    return GA_OK;
+}
+
+// The calling thread's side of such a walk (launched on wb.stream after the fill): decode the levels as
+// the progress word covers them, then the fill's cost, the walk's result words, the last levels, the
+// tails and the final random state
+int streamed_walk_finish(ga_ctx* c, const RngTable& R, const WalkBufs& wb, const WalkStart& st0, double t0,
+                         uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
+                         int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const int64_t m = c->m, n = c->n;
+    const int64_t nwords = (m + n + 1 + 15) / 16 + 64;
     WalkStart st = st0;
     int reason = 0;
     int64_t len = 0;
@@ -1400,6 +1399,26 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     const int rc = conclude_walk(R, st, reason, mt_state, a_chr, b_chr, oa, om, ob, cap, len, out_len, tb_status);
     c->call_ms = (float)(now_ms() - t0);
     return rc;
+}
+
+int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr, char* oa, char* om, char* ob,
+             int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
+    const double t0 = now_ms();
+    const int64_t m = c->m, n = c->n;
+    if (int r = rc_fill(c)) return r;
+    // the tie-break table on the host while the device fills
+    RngTable R;
+    const double t1 = now_ms();
+    build_rng(mt_state, m + n + 1, R);
+    c->rng_ms = (float)(now_ms() - t1);
+    WalkBufs wb = ctx_walk_bufs(c);
+    const int64_t ntab = (int64_t)R.tab.size();
+    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    // the walk's levels go to pinned host memory, and this thread decodes them while the walk runs
+    if (int r = pinned_walk_levels(c, wb)) return r;
+    const WalkStart st0{m, n, 0, 0, 0, 1};
+    if (int r = rc_walk_launch(c, ntab, st0, wb)) return r;
+    return streamed_walk_finish(c, R, wb, st0, t0, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
 }
 
 // ---------------------------------------------------------------- pipelined repeated alignments
@@ -2218,6 +2237,16 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     const double t1 = now_ms();
     build_rng(mt_state, c->m + c->n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
+    if (std::min(c->m, c->n) >= 256 && !getenv("GA_WALK_NOSTREAM")) {
+        // levels to pinned host memory, decoded while the walk runs (as rc_align; degenerate walks, which
+        // need a row or column of the matrix of length 1, keep the plain path)
+        WalkBufs wb = ctx_walk_bufs(c);
+        if (int r = pinned_walk_levels(c, wb)) return r;
+        const WalkStart st0{c->m, c->n, 0, 0, 0, 1};
+        if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), st0, 0, -1, false, true, &wb)) return r;
+        return streamed_walk_finish(c, R, wb, st0, t0, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status,
+                                    cost_out);
+    }
     if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), WalkStart{c->m, c->n, 0, 0, 0, 1})) return r;
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
     const int rc = finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
