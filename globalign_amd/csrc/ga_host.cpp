@@ -667,6 +667,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         if (tb || full || !lane_geometry(c, n, &qrows, false)) return fail(GA_E_STATE, "recompute fill needs the lane kernel");
         // the checkpointing variant runs 16-step sub-chunks (8 waves at TD = 8 would take 8-step ones)
         if (c->nwc == 8 && c->T == 8 && !lane_geometry(c, n, &qrows, false, 8, 4)) return fail(GA_E_STATE, "recompute fill geometry");
+        // the recompute workers stage a block's codes in LDS (64*TD columns x the checkpoint spacing): at
+        // wide stripes and wide spacings (C4: TD 8, every 256 steps, 219 KB) that exceeds the CU's LDS, so
+        // the stripes narrow until a worker fits beside the walk's 128 KB torus budget
+        constexpr int kRcLds = 256 * 256 * 2;  // the walk's torus (ga_walk.h TP x TP u16): the launch's dynamic LDS
+        while (c->T > 1 && 1024 + ga::rc_worker_bytes(c->T, c->CB, bd.rc_every) > kRcLds)
+            if (!lane_geometry(c, n, &qrows, false, c->T / 2, 4)) return fail(GA_E_STATE, "recompute fill geometry");
+        if (1024 + ga::rc_worker_bytes(c->T, c->CB, bd.rc_every) > kRcLds)
+            return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
         c->lane = true;
     } else if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
         c->lane = lane_geometry(c, n, &qrows, tb, bd.lane_td, bd.lane_nwc, 2048);
@@ -1151,8 +1159,10 @@ bool rc_eligible(ga_ctx* c) {
 int rc_every(ga_ctx* c) {
     int every = 64;
     if (const char* e = getenv("GA_RC_EVERY")) every = std::max(64, (atoi(e) / 32) * 32);
-    // memory: double the spacing until the states fit a budget (default 96 GB)
-    int64_t budget = (int64_t)96 << 30;
+    // memory: double the spacing until the states fit a budget (default 128 GB of the 288; the estimate
+    // below assumes one column per lane, twice what TD >= 2 stores: C4 on one GPU then takes a spacing of
+    // 128 steps, 78 GB at TD 4, walk 90 ms against 131 at 256, tools/exp/r3b_c4rc.py)
+    int64_t budget = (int64_t)128 << 30;
     if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
     const int64_t stripes = (c->n + 63) / 64;  // an upper bound at any TD: (TD + 1) / TD <= 2 per 64 columns
     while ((c->m / every) * stripes * 2 * 512 > budget && every < 4096) every *= 2;

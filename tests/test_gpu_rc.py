@@ -128,3 +128,11 @@ def test_rc_repeated_calls_reuse_buffers(monkeypatch):
             assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
     finally:
         eng.close()
+
+
+def test_rc_worker_lds_caps_stripe_width(monkeypatch):
+    """A block's staged codes must fit LDS: at 8 columns per lane and a 256-step checkpoint spacing (C4 on one GPU:
+    219 KB) the fill narrows its stripes (4 columns per lane, 113 KB) instead of failing the walk's launch."""
+    kind = _align(monkeypatch, splitmix_seq(3000, 31, "dna"), splitmix_seq(3100, 32, "dna"), DNA, seed=5,
+                  env={"GA_LANE_COLS_PER_LANE": 8, "GA_RC_EVERY": 256})
+    assert kind[1] == 4, kind
