@@ -12,10 +12,11 @@ Workloads (BASELINE.json configs, SURVEY 8d SplitMix64 inputs, resident in HBM):
                 repeated-pair pipeline is reported beside it as an extra key.  The N=1 line also carries "c4": one GPU's point of
                 the C4 scaling curve.
   c4 (default at N>1): 1M x 1M DNA, same scoring, score only.  BASELINE's 1/2/4/8-GPU scaling
-                config: the SAME pair for every N (strong scaling), cut into N column slabs whose
-                edges stream between GPUs in row bands over RCCL (globalign_amd/distributed.py).
-  c4tb:         C4 with full traceback on one GPU (banded: a checkpointing score pass, then band
-                refills + walk; 10^12 traceback bytes do not fit in HBM).
+                config: the SAME pair for every N (strong scaling), cut into N column slabs, each fill
+                storing its right edge into the next GPU's memory over xGMI (RCCL row bands as the
+                fallback; globalign_amd/distributed.py).
+  c4tb:         C4 with full traceback on one GPU (10^12 traceback bytes do not fit in HBM: the recompute
+                walk, a checkpointing score fill, then blocks recomputed beside the walk).
   c5:           20k x 20k protein (seeds 3, 4), BLOSUM62, gap_open_score -10, full traceback.
   c2:           10k x 10k DNA, full traceback.
   c1:           1k x 1k DNA (BASELINE configs[0], the reference's CPU-runnable case).
@@ -61,8 +62,8 @@ WORKLOADS = {
     "c4": dict(m=1_000_000, n=1_000_000, traceback=False, alphabet="dna", seeds=(1, 2), scoring=SCORING,
                desc=f"C4: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}, score only"),
     "c4tb": dict(m=1_000_000, n=1_000_000, traceback=True, alphabet="dna", seeds=(1, 2), scoring=SCORING, golden="c4",
-                 desc=f"C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}; banded "
-                      "traceback (checkpointed score pass + band refills, DESIGN.md 5.5)"),
+                 desc=f"C4 with full traceback: 1M x 1M DNA (SplitMix64 seeds 1,2), {DNA_SCORING_DESC}; recompute "
+                      "walk (checkpointing score fill, blocks recomputed beside the walk, DESIGN.md 5.8)"),
     # multi-rank rehearsal on ONE GPU only (tools/dist_rehearsal.sh): C4's rows, 16k columns, score only, so
     # that every rank's lane-kernel slab is resident beside the others' (not a BASELINE config)
     "c4r": dict(m=1_000_000, n=16_384, traceback=False, alphabet="dna", seeds=(1, 2), scoring=SCORING,

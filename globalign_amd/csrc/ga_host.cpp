@@ -626,7 +626,7 @@ struct Band {
     // the recompute walk's score fill: the lane kernel with its checkpoints (every stripe's
     // right edge, the staircase lane states every rc_every steps) into ctx->colck / ctx->stck
     bool rc = false;
-    int rc_every = 64;
+    int rc_every = 0;           // 0: chosen with the stripes' geometry (enqueue_fill)
     int2* ckpt = nullptr;       // checkpointing pass: where rows ckpt_rows, 2*ckpt_rows, ... go
     int ckpt_rows = 0;
     // pipelined alignments (align_many): a fill with buffers and a stream of its own, so that two
@@ -648,6 +648,7 @@ struct Band {
 
 // Enqueue boundary + query profile + fill.  Does not synchronise.
 int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
+    int every = bd.rc_every > 0 ? bd.rc_every : 64;  // the recompute fill's checkpoint spacing (chosen below)
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
     const bool tb = (flags & (GA_FILL_TRACEBACK | GA_FILL_FULL)) != 0;
     const bool full = (flags & GA_FILL_FULL) != 0;
@@ -671,10 +672,31 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // wide stripes and wide spacings (C4: TD 8, every 256 steps, 219 KB) that exceeds the CU's LDS, so
         // the stripes narrow until a worker fits beside the walk's 128 KB torus budget
         constexpr int kRcLds = 256 * 256 * 2;  // the walk's torus (ga_walk.h TP x TP u16): the launch's dynamic LDS
-        while (c->T > 1 && 1024 + ga::rc_worker_bytes(c->T, c->CB, bd.rc_every) > kRcLds)
+        // Stripes of at most 4 columns per lane (unless GA_LANE_COLS_PER_LANE asks): a block is 64 rows of one stripe, and the walk reads ~1-2 of
+        // its TD tiles, so wider blocks starve the walk (C4 on one GPU at TD 8: fill 226 ms, walk 160 ms;
+        // at TD 4: 284 + 90 ms, tools/exp/r3b_c4tb3.sh, r3b_c4rc.py)
+        if (c->T > 4 && !c->lane_T_req && !lane_geometry(c, n, &qrows, false, 4, 4))
+            return fail(GA_E_STATE, "recompute fill geometry");
+        // The checkpoint spacing, with the stripes' geometry known: the smallest (<= 4096 steps) whose states
+        // fit the memory budget (default 96 GB of the 288: C4 on one GPU, TD 4, takes 128 steps, 78 GB; 64
+        // would take 156 GB and walks no faster) and whose worker fits LDS; GA_RC_EVERY fixes it (the stripes
+        // narrow if it must)
+        int64_t budget = (int64_t)96 << 30;
+        if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
+        auto fits = [&](int e) {
+            const int64_t nck = std::max<int64_t>((m - 1) / e, 1);
+            return nck * c->nstripes * (c->T + 1) * 512 <= budget &&
+                   1024 + ga::rc_worker_bytes(c->T, c->CB, e) <= kRcLds;
+        };
+        for (;;) {
+            if (bd.rc_every > 0) every = bd.rc_every;
+            else
+                for (every = 64; every < 4096 && !fits(every); every *= 2) {}
+            if (1024 + ga::rc_worker_bytes(c->T, c->CB, every) <= kRcLds) break;
+            if (c->T == 1) return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
             if (!lane_geometry(c, n, &qrows, false, c->T / 2, 4)) return fail(GA_E_STATE, "recompute fill geometry");
-        if (1024 + ga::rc_worker_bytes(c->T, c->CB, bd.rc_every) > kRcLds)
-            return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
+        }
+        c->rc_every_used = every;
         c->lane = true;
     } else if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
         c->lane = lane_geometry(c, n, &qrows, tb, bd.lane_td, bd.lane_nwc, 2048);
@@ -752,9 +774,9 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (const char* e = getenv("GA_LANE_LATE")) p.late = atoi(e);
     p.hand_direct = 0;  // measured: C4 210 ms against 221 with the direct hand-off, 1M x 125k 52.5 against 56 (r3_c4.log)
     if (const char* e = getenv("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
-    p.stck_every = bd.rc_every;
+    p.stck_every = every;
     if (bd.rc) {
-        const int64_t nck = std::max<int64_t>((m - 1) / bd.rc_every, 1);
+        const int64_t nck = std::max<int64_t>((m - 1) / every, 1);
         HIPCHK(c->colck.ensure(sizeof(int2) * (size_t)c->nstripes * (m + 1)));
         HIPCHK(c->stck.ensure(sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64));
         p.colck = c->colck.as<int2>();
@@ -1155,29 +1177,21 @@ bool rc_eligible(ga_ctx* c) {
 }
 
 // checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps; wider
-// spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per spacing
-int rc_every(ga_ctx* c) {
-    int every = 64;
-    if (const char* e = getenv("GA_RC_EVERY")) every = std::max(64, (atoi(e) / 32) * 32);
-    // memory: double the spacing until the states fit a budget (default 128 GB of the 288; the estimate
-    // below assumes one column per lane, twice what TD >= 2 stores: C4 on one GPU then takes a spacing of
-    // 128 steps, 78 GB at TD 4, walk 90 ms against 131 at 256, tools/exp/r3b_c4rc.py)
-    int64_t budget = (int64_t)128 << 30;
-    if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
-    const int64_t stripes = (c->n + 63) / 64;  // an upper bound at any TD: (TD + 1) / TD <= 2 per 64 columns
-    while ((c->m / every) * stripes * 2 * 512 > budget && every < 4096) every *= 2;
-    return every;
+// The checkpoint spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per
+// spacing: chosen with the geometry in enqueue_fill; GA_RC_EVERY (a multiple of 32, >= 64) fixes it
+int rc_every_req() {
+    const char* e = getenv("GA_RC_EVERY");
+    return e ? std::max(64, (atoi(e) / 32) * 32) : 0;
 }
 
 // The score-only checkpointing fill of the loaded problem or slab.
 int rc_fill(ga_ctx* c) {
     Band bd;
     bd.rc = true;
-    bd.rc_every = rc_every(c);
+    bd.rc_every = rc_every_req();
     if (int r = enqueue_fill(c, 0, bd)) return r;
     c->rc_used = true;
     c->rc_T = c->T;
-    c->rc_every_used = bd.rc_every;
     return GA_OK;
 }
 
