@@ -1259,14 +1259,23 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
         // diagonal, dbi + dbs*TD + |dbi - dbs*TD|.  Only the first nwin are recomputed ahead (the walker's
         // own 2 x 2 tiles always rank first); speculative blocks cost the workers' time and the claims.
+        // Candidates up to 15 block rows / stripes away (4-bit offsets): a block written at offset d < 16 lands
+        // in the slot of the block 16 - d BELOW (right of) the walker's, which it has left, and two candidates
+        // never share a slot, so the 16 x 16-block cache still never overwrites a block the walker may read
+        // (the server's view of the walker's block may be stale, but only ever below it).  Deeper candidates
+        // keep the recompute ahead of a fast walker (C4, TD 4: a 28 us block against 27 us of walking across
+        // 8 block rows; round 3 first searched 8 x 8).
+        const int span = getenv("GA_RC_SPAN") ? std::max(2, std::min(16, atoi(getenv("GA_RC_SPAN")))) : 16;
         std::vector<std::pair<int, int>> off;
-        for (int di = 0; di < 8; di++)
-            for (int dj = 0; dj < 8; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
+        for (int di = 0; di < span; di++)
+            for (int dj = 0; dj < span; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
         std::stable_sort(off.begin(), off.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
             return x.second < y.second;
         });
         for (int k = 0; k < 64; k++) r.off[k] = (unsigned char)off[k].first;
-        r.nwin = 48;
+        // 64 of the 16 x 16 candidates (C3 walk 5.63 ms against 5.80 with 48 of 8 x 8, C4 with traceback 61 ms
+        // against 90: tools/exp/r3b_span.sh)
+        r.nwin = 64;
         if (const char* e = getenv("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
     }
     // recompute workgroups: with a faster walker (scalar entry loads) fewer workers keep up, and more of them
