@@ -8,6 +8,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout
 tail -2 $O/gpu_suite.txt
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" >> $O/gpu_suite.txt 2>&1 || { tail -5 $O/gpu_suite.txt; exit 1; }
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+timeout -k 10 400 python -u bench.py --workload c4tb --no-cpu-baseline --no-extra --steps 3 --warmup 1 > $O/bench_c4tb.json 2> $O/bench_c4tb.err || { tail -20 $O/bench_c4tb.err; exit 1; }
 for W in c5 c2; do
   timeout -k 10 200 python -u bench.py --workload $W --no-cpu-baseline --no-extra --steps 20 --warmup 5 > $O/bench_$W.json 2> $O/bench_$W.err || { tail -20 $O/bench_$W.err; exit 1; }
 done
