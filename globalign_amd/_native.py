@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("GA_LIB_PATH") or os.path.join(_HERE, "_lib", "libglob
 
 GA_FILL_TRACEBACK = 1
 GA_FILL_FULL = 2
+GA_E_NOMEM = -6
 GA_TB_OK = 0
 GA_TB_INDEX_ERROR = 1
 
@@ -138,6 +139,8 @@ def _check(rc):
         msg = _lib.ga_last_error().decode(errors="replace")
         if rc == -1:
             raise ValueError(msg)
+        if rc == GA_E_NOMEM:
+            raise MemoryError(f"globalign_amd engine: {msg}")
         raise EngineError(f"globalign_amd engine error {rc}: {msg}")
 
 
@@ -397,9 +400,16 @@ _default = {}
 _default_lock = threading.Lock()
 
 
+def knob_fingerprint():
+    """The GA_* overrides as the environment holds them now.  A context reads them once, when it is created
+    (ga_ctx_create), so cached engines are keyed by them: changing one (tests, tuning) gets a fresh context,
+    and a context's kernel choices never change under it."""
+    return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("GA_")))
+
+
 def default_engine(device=0):
-    """Process-wide engine per device (contexts are not thread-safe: one per thread)."""
-    key = (device, threading.get_ident())
+    """Process-wide engine per device and GA_* override set (contexts are not thread-safe: one per thread)."""
+    key = (device, threading.get_ident(), knob_fingerprint())
     with _default_lock:
         eng = _default.get(key)
         if eng is None:

@@ -49,6 +49,9 @@ struct FillArgs {
     int stck_every;           //   a multiple of 32 (a pair of 16-step sub-chunks)
     int late;                 // lane fill, score only: late edge reads (one-round chains; ga_lane.hip LATE)
     int hand_direct;          // lane fill: the last compute wave stores the hand-off rows (else the IO wave)
+    // tuning overrides from the context's knobs (ga_ctx::knobs; < 0: the default): LDS floor per workgroup
+    // (GA_FILL_LDS_FLOOR), lane-fill sub-chunk steps score only (GA_LANE_SUB) / with words (GA_LANE_TB_SUB)
+    int lds_floor, lane_sub, lane_tb_sub;
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),
@@ -86,9 +89,13 @@ struct WalkArgs {
 };
 
 // The recompute walk's tile cache: block (bi, bs) (64 rows of fill stripe bs) lives at slot
-// (bi mod RC_CACHE, bs mod RC_CACHE); the recompute window (8 x 8 blocks up-left of the walker) never
-// reaches a slot the walker may still read
-constexpr int RC_CACHE = 16;
+// (bi mod RC_CACHE_I, bs mod RC_CACHE_S).  Candidates lie at most RC_SPAN_MAX - 1 = 15 block rows / stripes
+// up-left of the walker's block as a worker saw it, and the cache is twice that deep on both axes: a worker
+// whose view of the walker is stale can then never overwrite a block the walker may still read (the safety
+// argument at rc_block's cache store, ga_rcwalk.hip; ADVICE r3: with a 16-deep cache it could)
+constexpr int RC_SPAN_MAX = 16;
+constexpr int RC_CACHE_I = 32;
+constexpr int RC_CACHE_S = 32;
 
 // The recompute workgroups of walk_rc_kernel (ga_rcwalk.hip): each wave recomputes 64-row
 // blocks of one fill stripe (64*TD columns) from the lane fill's checkpoints, writing their traceback words.

@@ -11,9 +11,11 @@
 //   * string assembly from the walk's per-step levels (take_* :688-753,
 //     the i==0 / j==0 tails :542-581 and the final reverse :584-586).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <chrono>
@@ -307,6 +309,14 @@ void state_after(const RngTable& R, int64_t D, uint32_t* out) {
 
 // ------------------------------------------------------------------ context
 struct ga_ctx {
+    // GA_* tuning / diagnostic overrides, snapshotted when the context is created (ga_ctx_create): a context's
+    // kernel choices never change under it, whatever the process does to its environment later.  knob("GA_X")
+    // is getenv's view of GA_X at that moment (nullptr: unset).
+    std::map<std::string, std::string> knobs;
+    const char* knob(const char* name) const {
+        const auto it = knobs.find(name);
+        return it == knobs.end() ? nullptr : it->second.c_str();
+    }
     int device = 0;
     int priority = 0;  // of `stream` (the greatest the device offers, see ga_ctx_create)
     hipStream_t stream = nullptr;
@@ -457,8 +467,8 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T
     static const double cyc1[4] = {84, 115, 154, 239};
     // workgroups per CU the residency check may count on (GA_LANE_WG_PER_CU, tuning: 2 needs an LDS floor
     // below 80 KB, GA_FILL_LDS_FLOOR)
-    static const int wpc = [] {
-        const char* e = getenv("GA_LANE_WG_PER_CU");
+    const int wpc = [c] {
+        const char* e = c->knob("GA_LANE_WG_PER_CU");
         return e ? std::max(1, std::min(2, atoi(e))) : 1;
     }();
     int64_t cus = c->num_cu * wpc;
@@ -502,8 +512,8 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T
     }
     if (!bestT) return false;
     // GA_LANE_QROWS caps the profile table (tuning: a smaller table lets two workgroups share a CU)
-    static const int qcap = [] {
-        const char* e = getenv("GA_LANE_QROWS");
+    const int qcap = [c] {
+        const char* e = c->knob("GA_LANE_QROWS");
         return e ? atoi(e) : 4096;
     }();
     const size_t budget = 150 * 1024;
@@ -681,11 +691,29 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // fit the memory budget (default 96 GB of the 288: C4 on one GPU, TD 4, takes 128 steps, 78 GB; 64
         // would take 156 GB and walks no faster) and whose worker fits LDS; GA_RC_EVERY fixes it (the stripes
         // narrow if it must)
+        // The budget is also capped by the device memory free for it: what hipMemGetInfo reports plus
+        // what this context's checkpoint buffers already hold, less the right-edge columns (8 B per row per
+        // stripe), the walk's tile cache and a 2 GB margin.  A problem whose checkpoints still do not fit returns
+        // GA_E_NOMEM, and ga_problem_align takes the banded traceback instead.
         int64_t budget = (int64_t)96 << 30;
-        if (const char* e = getenv("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
-        auto fits = [&](int e) {
+        if (const char* e = c->knob("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
+        int64_t dev_avail = INT64_MAX;
+        {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+                dev_avail = (int64_t)fr + (int64_t)c->stck.cap + (int64_t)c->colck.cap + (int64_t)c->rc_tb.cap -
+                            ((int64_t)2 << 30);
+        }
+        auto ck_bytes = [&](int e) {
             const int64_t nck = std::max<int64_t>((m - 1) / e, 1);
-            return nck * c->nstripes * (c->T + 1) * 512 <= budget &&
+            return nck * c->nstripes * (c->T + 1) * 512;
+        };
+        auto other_bytes = [&]() {
+            return (int64_t)c->nstripes * (m + 1) * 8 +
+                   (int64_t)ga::RC_CACHE_I * ga::RC_CACHE_S * c->T * 64 * 64 * c->CB + ((int64_t)64 << 20);
+        };
+        auto fits = [&](int e) {
+            return ck_bytes(e) <= std::min(budget, dev_avail - other_bytes()) &&
                    1024 + ga::rc_worker_bytes(c->T, c->CB, e) <= kRcLds;
         };
         for (;;) {
@@ -696,6 +724,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
             if (c->T == 1) return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
             if (!lane_geometry(c, n, &qrows, false, c->T / 2, 4)) return fail(GA_E_STATE, "recompute fill geometry");
         }
+        if (ck_bytes(every) > std::min(budget, dev_avail - other_bytes()))
+            return fail(GA_E_NOMEM, "recompute walk: the checkpoints do not fit the budget / free device memory");
         c->rc_every_used = every;
         c->lane = true;
     } else if (bd.lane_td > 0 && tb && !full && bd.ckpt == nullptr)
@@ -771,19 +801,29 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.stck = nullptr;
     // one round of lane workgroups (every stripe resident): the chain's lag counts, read edges late
     p.late = c->lane && c->nslabs <= c->num_cu ? 1 : 0;
-    if (const char* e = getenv("GA_LANE_LATE")) p.late = atoi(e);
+    if (const char* e = c->knob("GA_LANE_LATE")) p.late = atoi(e);
     p.hand_direct = 0;  // measured: C4 210 ms against 221 with the direct hand-off, 1M x 125k 52.5 against 56 (r3_c4.log)
-    if (const char* e = getenv("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
+    if (const char* e = c->knob("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
     p.stck_every = every;
+    {
+        const char* e = c->knob("GA_FILL_LDS_FLOOR");
+        p.lds_floor = e ? atoi(e) : -1;
+        e = c->knob("GA_LANE_SUB");
+        p.lane_sub = e ? atoi(e) : -1;
+        e = c->knob("GA_LANE_TB_SUB");
+        p.lane_tb_sub = e ? atoi(e) : -1;
+    }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);
-        HIPCHK(c->colck.ensure(sizeof(int2) * (size_t)c->nstripes * (m + 1)));
-        HIPCHK(c->stck.ensure(sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64));
+        for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * (size_t)c->nstripes * (m + 1)},
+                                  {&c->stck, sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64}})
+            if (const hipError_t e = buf->ensure(bytes); e != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(e == hipErrorOutOfMemory ? GA_E_NOMEM : GA_E_HIP,
+                            std::string("recompute checkpoints: ") + hipGetErrorString(e));
+            }
         p.colck = c->colck.as<int2>();
         p.stck = c->stck.as<int2>();
-        // (timing experiments only: leave one kind of checkpoint out; the walk is then wrong)
-        if (getenv("GA_RC_DBG_NOCOL")) p.colck = nullptr;
-        if (getenv("GA_RC_DBG_NOST")) p.stck_every = -1;
     }
     p.subp = c->qp.as<int>();
     p.K = c->K;
@@ -815,7 +855,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.cols_per_lane = c->T;
     p.spin_limit = 1u << 26;        // ~seconds: only a broken hand-off can reach it
     p.halo_spin_limit = 1u << 30;  // waiting on another GPU may take long (~30 s)
-    if (const char* e = getenv("GA_HALO_SPIN_LIMIT")) p.halo_spin_limit = (unsigned)std::max(1L, atol(e));  // (tests)
+    if (const char* e = c->knob("GA_HALO_SPIN_LIMIT")) p.halo_spin_limit = (unsigned)std::max(1L, atol(e));  // (tests)
     // a slab with a left neighbour: every wait of its fill is, in the end, a wait for that halo
     if (c->slab && c->col0 > 0) p.spin_limit = std::max(p.spin_limit, p.halo_spin_limit);
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
@@ -926,12 +966,12 @@ ga::WalkArgs walk_args(ga_ctx* c, int64_t ntab, const WalkStart& st, int64_t r0,
         // the loaders leave the 4x4 tile block's far off-diagonal corners: 28 % fewer
         // speculative tile loads, C3 walk 6.87 -> 6.71 ms alone and 7.74 -> 7.4 ms in the pipeline, C5
         // 1.45 -> 1.27 ms (tools/exp/walk_skip.sh); GA_WALK_SKIP_CORNERS = 0 / 2 / 3 for none / more
-        const char* e = getenv("GA_WALK_SKIP_CORNERS");
+        const char* e = c->knob("GA_WALK_SKIP_CORNERS");
         w.skip_corners = e ? atoi(e) : 1;
         // 14 loader waves (the L2 prefetcher's and the idle wave's too): tile waits at C3 469 -> 186 us
         // alone, 921 -> 413 us in the pipeline, walk 6.81 -> 6.52 ms alone, C5 1.28 -> 1.15 ms
         // (tools/exp/walk_loaders.sh); GA_WALK_LOADERS = 12 / 13 for the former roles
-        const char* nl = getenv("GA_WALK_LOADERS");
+        const char* nl = c->knob("GA_WALK_LOADERS");
         w.nloaders = nl ? atoi(nl) : 14;
     }
     w.ops = wb.ops;
@@ -1084,12 +1124,12 @@ int conclude_walk(const RngTable& snaps, const WalkStart& st, int reason, uint32
 // traceback words (its top row from the checkpoint) and the walk through it, handed on at the
 // band's top row (walk reason 6).  Fill work doubles; memory is one band of words.
 int64_t band_rows(ga_ctx* c) {
-    if (const char* e = getenv("GA_TB_BAND_ROWS")) {  // tests: force (small) bands
+    if (const char* e = c->knob("GA_TB_BAND_ROWS")) {  // tests: force (small) bands
         const int64_t Bh = (atoll(e) / ga::FROWS) * ga::FROWS;
         return Bh >= ga::FROWS && c->m >= 2 * Bh ? Bh : 0;
     }
     int64_t budget = (int64_t)64 << 30;
-    if (const char* e = getenv("GA_TB_BUDGET_MB")) budget = atoll(e) << 20;
+    if (const char* e = c->knob("GA_TB_BUDGET_MB")) budget = atoll(e) << 20;
     const int64_t words = ((c->n + 63) / 64) * 64 * c->CB;  // traceback bytes per row
     if (c->m * words <= budget) return 0;
     const int64_t Bh = std::max<int64_t>(64, (budget / words / ga::FROWS) * ga::FROWS);
@@ -1164,7 +1204,7 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
 // traceback words of the 64-row blocks ahead of it into a small tile cache.  The fill runs at score-only
 // speed and memory is O(checkpoints), not m*n words.
 bool rc_eligible(ga_ctx* c) {
-    const char* e = getenv("GA_RC");  // 0: never; 1: whenever the shape allows (tests); default: large problems
+    const char* e = c->knob("GA_RC");  // 0: never; 1: whenever the shape allows (tests); default: large problems
     const int mode = e ? atoi(e) : -1;
     if (mode == 0 || c->slab || c->qbytes != 1 || c->K > 32) return false;
     if (c->m < 256 || c->n < 256) return false;  // (degenerate walks read cells no block ever recomputes)
@@ -1172,15 +1212,15 @@ bool rc_eligible(ga_ctx* c) {
     // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
     // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
     int64_t min_cells = (int64_t)1 << 32;
-    if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
+    if (const char* t = c->knob("GA_RC_MIN_CELLS")) min_cells = atoll(t);
     return c->m * c->n >= min_cells;
 }
 
 // checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps; wider
 // The checkpoint spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per
 // spacing: chosen with the geometry in enqueue_fill; GA_RC_EVERY (a multiple of 32, >= 64) fixes it
-int rc_every_req() {
-    const char* e = getenv("GA_RC_EVERY");
+int rc_every_req(const ga_ctx* c) {
+    const char* e = c->knob("GA_RC_EVERY");
     return e ? std::max(64, (atoi(e) / 32) * 32) : 0;
 }
 
@@ -1188,7 +1228,7 @@ int rc_every_req() {
 int rc_fill(ga_ctx* c) {
     Band bd;
     bd.rc = true;
-    bd.rc_every = rc_every_req();
+    bd.rc_every = rc_every_req(c);
     if (int r = enqueue_fill(c, 0, bd)) return r;
     c->rc_used = true;
     c->rc_T = c->T;
@@ -1201,7 +1241,8 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     const int64_t m = c->m, n = c->n;
     const int TD = c->rc_T, CB = c->CB;
     const int nbi = (int)((m + 63) / 64), nbs = c->nstripes;
-    HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE * ga::RC_CACHE * TD * 64 * 64 * CB));
+    // (+ one 64-column stripe of slack: a loader reads whole 1 KiB runs)
+    HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4));
     const size_t nflags = (size_t)nbi * nbs;
     if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_epoch >= 0x7ffffff0u) {
         HIPCHK(c->rc_flags.ensure(nflags * sizeof(unsigned)));
@@ -1213,11 +1254,11 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, wb.stream));
     wb.tb = c->rc_tb.as<uint8_t>();
     ga::WalkArgs w = walk_args(c, ntab, st, 0, -1, false, wb);
-    w.TC = ga::RC_CACHE * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
+    w.TC = ga::RC_CACHE_I * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
     // 14 loaders, no L2 prefetcher (it would read blocks not yet recomputed); GA_RC_LOADERS = 12 / 13 leave
     // waves 8 and 12 / wave 8 (the walker's SIMD) idle instead
     w.nloaders = 14;
-    if (const char* e = getenv("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
+    if (const char* e = c->knob("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
     w.rc_flags = c->rc_flags.as<unsigned>();
     w.rc_ready = 2u * c->rc_epoch + 1u;
     w.rc_nbs = nbs;
@@ -1251,7 +1292,7 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     // one worker per workgroup (one per CU) by default: C3 blocks 14.7 us against 16.5 at three per CU,
     // the walker's tile waits 0.07 against 0.5 ms (tools/exp/r3_rc_diag.py)
     r.workers = std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
-    if (const char* e = getenv("GA_RC_WPW")) r.workers = std::max(1, std::min(r.workers, atoi(e)));
+    if (const char* e = c->knob("GA_RC_WPW")) r.workers = std::max(1, std::min(r.workers, atoi(e)));
     else r.workers = 1;
     r.spin_limit = 1u << 20;
     {
@@ -1259,13 +1300,12 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
         // diagonal, dbi + dbs*TD + |dbi - dbs*TD|.  Only the first nwin are recomputed ahead (the walker's
         // own 2 x 2 tiles always rank first); speculative blocks cost the workers' time and the claims.
-        // Candidates up to 15 block rows / stripes away (4-bit offsets): a block written at offset d < 16 lands
-        // in the slot of the block 16 - d BELOW (right of) the walker's, which it has left, and two candidates
-        // never share a slot, so the 16 x 16-block cache still never overwrites a block the walker may read
-        // (the server's view of the walker's block may be stale, but only ever below it).  Deeper candidates
-        // keep the recompute ahead of a fast walker (C4, TD 4: a 28 us block against 27 us of walking across
-        // 8 block rows; round 3 first searched 8 x 8).
-        const int span = getenv("GA_RC_SPAN") ? std::max(2, std::min(16, atoi(getenv("GA_RC_SPAN")))) : 16;
+        // Candidates up to 15 block rows / stripes away (4-bit offsets) in a cache 32 deep on both axes (the
+        // safety argument is at rc_block's cache store, ga_rcwalk.hip).  Deeper candidates keep the recompute
+        // ahead of a fast walker (C4, TD 4: a 28 us block against 27 us of walking across 8 block rows; round 3
+        // first searched 8 x 8).
+        const int span = c->knob("GA_RC_SPAN") ? std::max(2, std::min(ga::RC_SPAN_MAX, atoi(c->knob("GA_RC_SPAN"))))
+                                               : ga::RC_SPAN_MAX;
         std::vector<std::pair<int, int>> off;
         for (int di = 0; di < span; di++)
             for (int dj = 0; dj < span; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
@@ -1276,13 +1316,13 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         // 64 of the 16 x 16 candidates (C3 walk 5.63 ms against 5.80 with 48 of 8 x 8, C4 with traceback 61 ms
         // against 90: tools/exp/r3b_span.sh)
         r.nwin = 64;
-        if (const char* e = getenv("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
+        if (const char* e = c->knob("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
     }
     // recompute workgroups: with a faster walker (scalar entry loads) fewer workers keep up, and more of them
     // slow the walker's own tile loads (C3 walk 5.78 / 5.84 / 5.99 / 6.24 ms at 48 / 64 / 96 / 128 workers,
     // 6.05 at 40, 6.72 at 32: tools/exp/r3b_servers.sh); 64 keeps a margin above the cliff
     int nserv = 64;
-    if (const char* e = getenv("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
+    if (const char* e = c->knob("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
     HIPCHK(hipEventRecord(wb.ev0, wb.stream));
     ga::launch_walk_rc(wb.stream, w, r, nserv);
     HIPCHK(hipGetLastError());
@@ -1292,14 +1332,14 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
 
 // a slab's traceback fill (ga_slab_fill_launch): the same rule on the slab's own columns
 bool rc_slab_eligible(ga_ctx* c) {
-    const char* e = getenv("GA_RC");
+    const char* e = c->knob("GA_RC");
     const int mode = e ? atoi(e) : -1;
     if (mode == 0 || c->qbytes != 1 || c->K > 32 || c->m < 256 || c->n < 256) return false;
     if (mode == 1) return true;
     // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
     // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
     int64_t min_cells = (int64_t)1 << 32;
-    if (const char* t = getenv("GA_RC_MIN_CELLS")) min_cells = atoll(t);
+    if (const char* t = c->knob("GA_RC_MIN_CELLS")) min_cells = atoll(t);
     return c->m * c->n >= min_cells;
 }
 
@@ -1364,12 +1404,12 @@ int streamed_walk_finish(ga_ctx* c, const RngTable& R, const WalkBufs& wb, const
                 L = (int)lv;
             }
         };
-        static const int64_t lag = [] {
-            const char* e = getenv("GA_RC_DECODE_LAG");  // (diagnostics) blocks of 512 dispatches held back
+        const int64_t lag = [c] {
+            const char* e = c->knob("GA_RC_DECODE_LAG");  // (diagnostics) blocks of 512 dispatches held back
             return e ? (int64_t)atoi(e) * 512 : (int64_t)0;
         }();
         std::vector<uint32_t> seen;  // (diagnostics) GA_RC_DECODE_CHECK: the words as decoded
-        const bool check = getenv("GA_RC_DECODE_CHECK") != nullptr;
+        const bool check = c->knob("GA_RC_DECODE_CHECK") != nullptr;
         if (check) seen.assign((size_t)nwords, 0u);
         for (;;) {
             const unsigned pr = __atomic_load_n(c->rc_ops_prog, __ATOMIC_ACQUIRE);
@@ -1471,7 +1511,7 @@ int pipe_setup(ga_ctx* c) {
         // masked out of the fill streams it never waits for one to drain, and two fills may share the
         // other CUs (GA_PIPE_WALK_CUS, default 0: unmasked streams)
         int wc = 0;
-        if (const char* e = getenv("GA_PIPE_WALK_CUS")) wc = std::max(0, std::min(8, atoi(e)));
+        if (const char* e = c->knob("GA_PIPE_WALK_CUS")) wc = std::max(0, std::min(8, atoi(e)));
         c->walk_cus = wc;
         if (wc > 0) {
             const int nc = c->num_cu, words = (nc + 31) / 32;
@@ -1593,9 +1633,7 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
     if (!c->cwstream) {
         int lo = 0, hi = 0;
         HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        const char* pe = getenv("GA_CHAIN_PRIO");  // experiments: hi / normal
-        const int pr = pe && !strcmp(pe, "hi") ? hi : pe && !strcmp(pe, "normal") ? 0 : lo;
-        HIPCHK(hipStreamCreateWithPriority(&c->cwstream, hipStreamNonBlocking, pr));
+        HIPCHK(hipStreamCreateWithPriority(&c->cwstream, hipStreamNonBlocking, lo));
     }
     hipStream_t ws = c->cwstream;
     const int64_t need = (int64_t)count * per;
@@ -1723,12 +1761,6 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
         ga::launch_walk_chain(ws, A);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(c->pipe[0].w1, ws));
-        if (const char* e = getenv("GA_CHAIN_STAGGER"); e && atoi(e) > 0) {
-            // experiment: fill 0 alone on the chip, the others after it (the first walk starts sooner)
-            HIPCHK(hipEventSynchronize(c->pipe[0].fdone));
-            signalled = 1;
-            __atomic_store_n(ctl, 1u, __ATOMIC_RELEASE);
-        }
         for (int k = 1; k < std::min(count, S); k++) {
             if (int r = pipe_fill(c, k, fs[k % F])) return r;
             enqueued++;
@@ -1737,7 +1769,7 @@ int align_chain(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, con
     };
     if (int r = launch_all()) return stop(r);
     FILE* trace = nullptr;
-    if (const char* tp = getenv("GA_PIPE_TRACE")) trace = fopen(tp, "a");
+    if (const char* tp = c->knob("GA_PIPE_TRACE")) trace = fopen(tp, "a");
     const double h0 = now_ms();
     int64_t G = 0;
     float fill_sum = 0.f, walk_sum = 0.f;
@@ -1831,7 +1863,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // (8.65 ms per alignment; tools/exp/pipe_lane2.sh).  So one-byte words of long rows (K <= 32,
         // an int8 profile) take lane fills; the rest three row-scan fills.  GA_PIPE_MODE=row|lane
         // and GA_PIPE_FILLS (2..4) override.
-        const char* pm = getenv("GA_PIPE_MODE");
+        const char* pm = c->knob("GA_PIPE_MODE");
         bool lane = c->CB == 1 && c->qbytes == 1 && c->K <= 32 && c->m >= 32768 && c->n >= 4 * 4 * 64 * 64 &&
                     c->diag_req != 1 && c->diag_req != 2;
         if (pm && !strcmp(pm, "row")) lane = false;
@@ -1846,12 +1878,12 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // row-scan fills: three in flight (four streams with the walk's: HIP's default pool holds them);
         // with the faster walk C5 is no longer walk-bound (1.80 -> 1.51 ms per alignment), C2 unchanged
         int F = lane ? (queues >= 5 ? 4 : 3) : 3;
-        if (const char* e = getenv("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
+        if (const char* e = c->knob("GA_PIPE_FILLS")) F = std::max(2, std::min(4, atoi(e)));
         c->pipe_fills = F;
         // slots: fill k + S reuses walk k's buffers, so the walk chain allows one alignment per
         // (walk + fill) / S; GA_PIPE_SLOTS raises S above F + 1 (up to 6)
         int S = F + 1;
-        if (const char* e = getenv("GA_PIPE_SLOTS")) S = std::max(F + 1, std::min(6, atoi(e)));
+        if (const char* e = c->knob("GA_PIPE_SLOTS")) S = std::max(F + 1, std::min(6, atoi(e)));
         c->pipe_slots = S;
     }
     if (int r = pipe_setup(c)) return r;
@@ -1863,10 +1895,10 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         // host-written words, so a device-synchronising call another thread of the process makes while it
         // runs (hipFree, hipDeviceSynchronize, a torch allocator release) would wait on it until its 60 s
         // bound; per-launch walks have no such hazard and cost C2 / C5 ~1-10 % more per alignment.
-        const char* ch = getenv("GA_PIPE_CHAIN");
+        const char* ch = c->knob("GA_PIPE_CHAIN");
         const bool fits = (int64_t)count * (c->m + c->n + 1) <= ((int64_t)256 << 20);  // 1 GB of entries
         const bool on = ch != nullptr && atoi(ch) != 0;
-        if (on && fits && c->walk_cus == 0 && !getenv("GA_PIPE_FILL_PRIO") && !getenv("GA_PIPE_ROW_FIRST"))
+        if (on && fits && c->walk_cus == 0 && !c->knob("GA_PIPE_FILL_PRIO") && !c->knob("GA_PIPE_ROW_FIRST"))
             return align_chain(c, count, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out, t0);
     }
     const int64_t m = c->m, n = c->n, per = m + n + 1;
@@ -1876,7 +1908,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     if (c->walk_cus > 0) {
         for (int f = 0; f < 4; f++) fs[f] = c->mfstream[f];
         ws = c->mwstream;
-    } else if (const char* fp = getenv("GA_PIPE_FILL_PRIO"); fp && !strcmp(fp, "normal")) {
+    } else if (const char* fp = c->knob("GA_PIPE_FILL_PRIO"); fp && !strcmp(fp, "normal")) {
         for (int f = 0; f < 4; f++) {
             if (!c->nfstream[f]) HIPCHK(hipStreamCreateWithPriority(&c->nfstream[f], hipStreamNonBlocking, 0));
             fs[f] = c->nfstream[f];
@@ -1892,7 +1924,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
             if (origin) (void)hipEventDestroy(origin);
         }
     } tr;
-    if (const char* tp = getenv("GA_PIPE_TRACE"))
+    if (const char* tp = c->knob("GA_PIPE_TRACE"))
         if (hipEventCreate(&tr.origin) == hipSuccess && hipEventRecord(tr.origin, fs[0]) == hipSuccess)
             tr.f = fopen(tp, "a");
     FILE* const trace = tr.f;
@@ -1901,14 +1933,14 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     double walk_launch_host = 0.0;
     // experiment (GA_PIPE_ROW_FIRST=r): the first r fills through the row scan (shorter latency alone)
     int row_first = 0;
-    if (const char* e = getenv("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
+    if (const char* e = c->knob("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
     // fill j into slot j % S on fill stream j % F; each computes its own boundary.  Every fill of the
     // pipeline computes the same arrays (the same pair, boundary and words), so walk k takes whichever
     // pending slot's fill ended first, not slot k % S: in the ramp the third of four fills started at
     // once ends ~3 ms after the fourth and ~3 ms after the third walk wanted it (GA_PIPE_SLOT_ORDER=fixed
     // keeps slot k % S)
-    const bool any_order = [] {
-        const char* e = getenv("GA_PIPE_SLOT_ORDER");
+    const bool any_order = [c] {
+        const char* e = c->knob("GA_PIPE_SLOT_ORDER");
         return !(e && !strcmp(e, "fixed"));
     }();
     size_t io_stride = 0;
@@ -1916,8 +1948,8 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     if (int r = pipe_io(c, S, &io_stride, &io_dev)) return r;
     // slot s's walk writes its result words and levels to pinned memory (pipe_io; GA_PIPE_PINNED_IO=0:
     // to the slot's device buffers, read back with hipMemcpy)
-    const bool pinned_io = [] {
-        const char* e = getenv("GA_PIPE_PINNED_IO");
+    const bool pinned_io = [c] {
+        const char* e = c->knob("GA_PIPE_PINNED_IO");
         return !(e && atoi(e) == 0);
     }();
     auto walk_bufs = [&](int s) {
@@ -2115,6 +2147,9 @@ int ga_ctx_create(int device, ga_ctx** out) {
     HIPCHK(hipSetDevice(device));
     ga_ctx* c = new ga_ctx();
     c->device = device;
+    for (char** e = environ; e && *e; e++)  // the GA_* overrides, once (ga_ctx::knobs)
+        if (!strncmp(*e, "GA_", 3))
+            if (const char* eq = strchr(*e, '=')) c->knobs[std::string(*e, (size_t)(eq - *e))] = eq + 1;
     {
         // hardware queues per priority pool: what the HIP runtime read when it started, i.e. the variable
         // as the process first saw it here (a later change, e.g. a module setting it after HIP started,
@@ -2129,12 +2164,12 @@ int ga_ctx_create(int device, ga_ctx** out) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             c->num_cu = cus;
-        if (const char* e = getenv("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
-        if (const char* e = getenv("GA_FILL_NWC")) c->nwc_req = atoi(e);
-        if (const char* e = getenv("GA_FILL_MODE"))
+        if (const char* e = c->knob("GA_COLS_PER_LANE")) c->T_req = atoi(e);  // tuning overrides
+        if (const char* e = c->knob("GA_FILL_NWC")) c->nwc_req = atoi(e);
+        if (const char* e = c->knob("GA_FILL_MODE"))
             c->diag_req = !strcmp(e, "diag") ? 2 : !strcmp(e, "row") ? 1 : !strcmp(e, "lane") ? 3 : 0;
-        if (const char* e = getenv("GA_LANE_COLS_PER_LANE")) c->lane_T_req = atoi(e);
-        if (const char* e = getenv("GA_DIAG_COLS_PER_LANE")) c->diag_T_req = atoi(e);
+        if (const char* e = c->knob("GA_LANE_COLS_PER_LANE")) c->lane_T_req = atoi(e);
+        if (const char* e = c->knob("GA_DIAG_COLS_PER_LANE")) c->diag_T_req = atoi(e);
     }
     // The fill runs on a stream of the greatest priority.  HIP keeps a separate pool of hardware
     // queues per priority (GPU_MAX_HW_QUEUES = 4 per pool and process), so no normal-priority
@@ -2143,7 +2178,7 @@ int ga_ctx_create(int device, ga_ctx** out) {
     // (DESIGN.md 7).  GA_STREAM_PRIORITY=normal restores a default-priority stream (experiments).
     {
         int lo = 0, hi = 0;
-        const char* pe = getenv("GA_STREAM_PRIORITY");
+        const char* pe = c->knob("GA_STREAM_PRIORITY");
         const bool normal = pe && !strcmp(pe, "normal");
         if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
         c->priority = normal ? 0 : hi;  // 0: the default priority (lo is the LEAST, another pool)
@@ -2260,7 +2295,12 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     if (c->slab) return fail(GA_E_STATE, "slab contexts use ga_slab_fill_launch");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
     c->rc_used = false;
-    if (rc_eligible(c)) return rc_align(c, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
+    if (rc_eligible(c)) {
+        const int r = rc_align(c, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
+        // checkpoints that do not fit this device (nothing was enqueued): the banded traceback below
+        if (r != GA_E_NOMEM) return r;
+        c->rc_used = false;
+    }
     if (const int64_t Bh = band_rows(c)) return banded_align(c, Bh, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len,
                                                              tb_status, cost_out);
     const double t0 = now_ms();
@@ -2270,7 +2310,7 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     const double t1 = now_ms();
     build_rng(mt_state, c->m + c->n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
-    if (std::min(c->m, c->n) >= 256 && !getenv("GA_WALK_NOSTREAM")) {
+    if (std::min(c->m, c->n) >= 256 && !c->knob("GA_WALK_NOSTREAM")) {
         // levels to pinned host memory, decoded while the walk runs (as rc_align; degenerate walks, which
         // need a row or column of the matrix of length 1, keep the plain path)
         WalkBufs wb = ctx_walk_bufs(c);

@@ -1326,11 +1326,7 @@ static void launch_one(hipStream_t s, const FillArgs& p) {
     if constexpr (!DBG && CB == 1 && std::is_same<QT, int8_t>::value && !FULL)
         if (p.dbg != nullptr) return launch_one<CB, QT, TB, FULL, NWC, T, true>(s, p);
     // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
-    static const long floor_env = [] {
-        const char* e = getenv("GA_FILL_LDS_FLOOR");
-        return e ? atol(e) : -1L;
-    }();
-    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t floor_b = p.lds_floor >= 0 ? (size_t)p.lds_floor : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(
         fill_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows, TB ? TbStage<CB, T>::UINT4S * 16 : 0), floor_b);
     auto* fn = fill_kernel<CB, QT, TB, FULL, NWC, T, DBG>;
@@ -1383,11 +1379,7 @@ size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows) {
 template <typename QT, int NWC, int TD, bool FULL, bool DBG = false>
 static void launch_diag_one(hipStream_t s, const FillArgs& p) {
     if (!DBG && p.dbg != nullptr) return launch_diag_one<QT, NWC, TD, FULL, true>(s, p);
-    static const long floor_env = [] {
-        const char* e = getenv("GA_FILL_LDS_FLOOR");
-        return e ? atol(e) : -1L;
-    }();
-    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t floor_b = p.lds_floor >= 0 ? (size_t)p.lds_floor : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_diag_lds_bytes(NWC, (int)sizeof(QT), p.K, p.qrows), floor_b);
     auto* fn = fill_diag_kernel<QT, NWC, TD, FULL, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

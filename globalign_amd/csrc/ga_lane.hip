@@ -521,14 +521,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
 
 template <int NWC, int TD, int CB, int SUB, bool DBG = false>
 static void launch_lane_one(hipStream_t s, const FillArgs& p) {
+    // the recompute checkpoints exist in one variant only (no timestamps, 16-step sub-chunks): enqueue_fill
+    // asks for nothing else with them, and any other variant would leave them unwritten
+    if constexpr (CB == 0 && SUB != 16)
+        if (p.stck != nullptr) return launch_lane_one<NWC, TD, CB, 16, false>(s, p);
     if constexpr (!DBG && CB == 0)
-        if (p.dbg != nullptr) return launch_lane_one<NWC, TD, CB, SUB, true>(s, p);
+        if (p.dbg != nullptr && p.stck == nullptr) return launch_lane_one<NWC, TD, CB, SUB, true>(s, p);
     // the LDS floor sets how many workgroups share a CU (GA_FILL_LDS_FLOOR overrides it, for tuning)
-    static const long floor_env = [] {
-        const char* e = getenv("GA_FILL_LDS_FLOOR");
-        return e ? atol(e) : -1L;
-    }();
-    const size_t floor_b = floor_env >= 0 ? (size_t)floor_env : (size_t)FILL_LDS_MIN;
+    const size_t floor_b = p.lds_floor >= 0 ? (size_t)p.lds_floor : (size_t)FILL_LDS_MIN;
     const size_t lds = std::max<size_t>(fill_lane_lds_bytes(NWC, p.K, p.qrows), floor_b);
     if constexpr (CB == 0 && !DBG && SUB == 16) {
         if (p.stck != nullptr) {
@@ -571,12 +571,8 @@ static void launch_lane_td(hipStream_t s, const FillArgs& p) {
     // score only: 16-step sub-chunks (GA_LANE_SUB=8 selects 8, for tuning); traceback words: 16-step
     // sub-chunks for one-byte words at TD <= 4 with 4 waves (202 VGPRs, no spills; the pipelined C3 fill
     // 26.2 -> 24.9 ms, 8.85 -> 8.34 ms per alignment in steady state; GA_LANE_TB_SUB=8 selects 8), else 8
-    static const int sub_env = [] {
-        const char* e = getenv("GA_LANE_SUB");
-        return e ? atoi(e) : 16;
-    }();
-    const char* tbe = getenv("GA_LANE_TB_SUB");  // read per launch (tests switch it)
-    const int tb_sub_env = tbe ? atoi(tbe) : 16;
+    const int sub_env = p.lane_sub > 0 ? p.lane_sub : 16;
+    const int tb_sub_env = p.lane_tb_sub > 0 ? p.lane_tb_sub : 16;
     // (TD = 8 at 8 waves per workgroup spills with 16-step sub-chunks: 8)
     constexpr bool tb16 = CB == 1 && TD <= 4;
     if constexpr (tb16) {

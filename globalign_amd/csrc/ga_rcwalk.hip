@@ -12,8 +12,8 @@
 //                 stripe's 64*TD columns), stages the cells' traceback codes in LDS and writes the block's
 //                 words into the cache with write-through (sc1) stores, then the flag.
 // A block is 64 rows of one fill stripe: TD walker tiles.  The walk path only moves up and left, so the
-// window (8 x 8 blocks up-left of the walker's block) always holds the tiles it can reach next, and a
-// 16 x 16-block cache never overwrites a block the walker may still read.  The words are the ones the
+// window (up to 16 x 16 blocks up-left of the walker's block) always holds the tiles it can reach next, and a
+// 32 x 32-block cache never overwrites a block the walker may still read.  The words are the ones the
 // full traceback fill writes (lk_code of the same exact int32 cells), so the walk is unchanged.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -155,13 +155,26 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    // the cache: block (bi, bs) at slot (bi mod RC_CACHE, bs mod RC_CACHE); TC words per lane per 64-column
-    // stripe of the cache (RC_CACHE * 4 * CB)
+    // The cache: block (bi, bs) at slot (bi mod RC_CACHE_I, bs mod RC_CACHE_S); TC words per lane per 64-column
+    // stripe of the cache (RC_CACHE_I * 4 * CB).  Only a block the walker can still reach is written: the walk
+    // moves up and left and its loaders read tiles of the 4 x 4 block at its tile, so a block below the
+    // walker's tile row, or right of its tile column, is never read again.  Safety: a block Y written now passed
+    // this check, so at this moment the walker's block row V is >= Y.  A block X sharing Y's slot (X = Y - 32k
+    // above it; the column axis is the same) is claimed only from a view V' of the walker with X >= V' - 15,
+    // i.e. V' <= Y - 17: after the walker has moved >= 17 block rows (>= 1088 steps, tens of us) past where it
+    // is now.  Y's stores issued here drain (vmcnt(0), rc_server) long before, so X's words, written after X's
+    // recompute, are the slot's last.  (With a 16-deep cache and 16-deep candidates the margin was zero, and
+    // two workers with different views could leave the walker another block's words)
+    {
+        const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
+        const int tile = pv ? (int)(pv - 1u) : r.tile0;
+        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return;  // out of reach: nobody reads it
+    }
 #pragma unroll
     for (int p = 0; p < TD; p++) {
         const uint4* src = reinterpret_cast<const uint4*>(stage + (p * 64 + lane) * SP + (R0 - t0 + 64) * CB);  // row R0+1
         uint4* dst = reinterpret_cast<uint4*>(r.tb) +
-                     ((long long)((bs % RC_CACHE) * TD + p) * r.TC + (bi % RC_CACHE) * 4 * CB) * 64 + lane;
+                     ((long long)((bs % RC_CACHE_S) * TD + p) * r.TC + (bi % RC_CACHE_I) * 4 * CB) * 64 + lane;
 #pragma unroll
         for (int d = 0; d < 4 * CB; d++) st16_sc1(dst + d * 64, src[d]);
     }

@@ -128,8 +128,8 @@ __device__ void load_tile(const WalkArgs& w, int ti, int tj, uint16_t* torus, ui
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const int bj = colok ? w.b[j - 1] : 0xfe;
-    // RC: the recompute walk's tile cache (ga_rcwalk.hip): block row ti mod RC_CACHE, fill stripe tj / td mod RC_CACHE
-    const int tic = RC ? ti % RC_CACHE : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE) * w.rc_td + tj % w.rc_td : tj;
+    // RC: the recompute walk's tile cache (ga_rcwalk.hip): block row ti mod RC_CACHE_I, fill stripe tj / td mod RC_CACHE_S
+    const int tic = RC ? ti % RC_CACHE_I : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE_S) * w.rc_td + tj % w.rc_td : tj;
     const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tjc * w.TC + tic * KW) * 64 + lane;
     const int nq = min(KW, w.TC - ti * KW);
     uint4 ch[KW];
@@ -184,7 +184,7 @@ __device__ inline void load_tile_b1(const WalkArgs& w, int ti, int tj, uint16_t*
     sa[lane] = (i0 + lane <= w.m) ? w.a[i0 + lane - 1] : 0xff;
     const bool colok = j <= w.n;
     const unsigned bj = colok ? w.b[j - 1] : 0xfeu;
-    const int tic = RC ? ti % RC_CACHE : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE) * w.rc_td + tj % w.rc_td : tj;
+    const int tic = RC ? ti % RC_CACHE_I : ti, tjc = RC ? ((tj / w.rc_td) % RC_CACHE_S) * w.rc_td + tj % w.rc_td : tj;
     const uint4* base = reinterpret_cast<const uint4*>(w.tb) + ((long long)tjc * w.TC + tic * 4) * 64 + lane;
     const int nq = w.TC - ti * 4;
     unsigned wv[16];

@@ -236,10 +236,22 @@ def link_ipc(dist, links, engine):
     importer launches its fill only after receiving it, so a fill never writes an edge its reader is still
     reading from the previous problem (that reader exports only when it starts the next)."""
     rank, world = links.rank, links.world
+    err = None
     if rank > 0:
-        _send_obj(dist, engine.slab_link_export(), rank - 1, links.ctrl)
+        # a failed export still sends (None): rank - 1 must not wait for a handle that never comes (ADVICE r3)
+        try:
+            handle = engine.slab_link_export()
+        except Exception as e:  # noqa: BLE001 (re-raised below, after the matching send)
+            handle, err = None, e
+        _send_obj(dist, handle, rank - 1, links.ctrl)
     if rank < world - 1:
-        engine.slab_link_import(_recv_obj(dist, rank + 1, links.ctrl))
+        handle = _recv_obj(dist, rank + 1, links.ctrl)
+        if handle is None:
+            err = err or RuntimeError(f"rank {rank + 1} could not export its edge buffer")
+        elif err is None:
+            engine.slab_link_import(handle)
+    if err is not None:
+        raise err
 
 
 def _send_obj(dist, obj, dst, group):
@@ -343,7 +355,8 @@ _device_engines_lock = threading.Lock()
 def device_engines(devices):
     """The slab engines of GlobalAligner(devices=...), one context per listed device, kept for the process
     (per thread: contexts are not thread-safe) so repeated calls reuse their buffers and linked halos."""
-    key = (tuple(devices), threading.get_ident())
+    from globalign_amd import _native
+    key = (tuple(devices), threading.get_ident(), _native.knob_fingerprint())
     with _device_engines_lock:
         engines = _device_engines.get(key)
         if engines is None:

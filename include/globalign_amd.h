@@ -27,6 +27,7 @@ extern "C" {
 #define GA_E_RANGE -3    /* int32 range / size limit exceeded               */
 #define GA_E_STATE -4    /* call order violated (e.g. traceback before fill) */
 #define GA_E_TIMEOUT -5  /* a device-side wait exceeded its spin bound      */
+#define GA_E_NOMEM -6    /* device memory too small for the chosen path      */
 
 /* Python-visible outcome of a traceback (dp_array_backward semantics). */
 #define GA_TB_OK 0

@@ -248,3 +248,53 @@ def test_slab_bounds_and_bands():
     assert bl[0] == (1, 512) and bl[1] == (513, 1536) and bl[-1][1] == 100_000
     assert all(b[0] == a[1] + 1 for a, b in zip(bl, bl[1:])) and max(r1 - r0 + 1 for r0, r1 in bl) == 8192
     assert bands(7, 8192) == [(1, 7)]
+
+
+class _LinkOnlyEngine:
+    """Just the IPC link half of the slab interface: rank `bad` cannot export its edge buffer."""
+
+    def __init__(self, rank, bad):
+        self.rank, self.bad, self.imported = rank, bad, None
+
+    def slab_link_export(self):
+        if self.rank == self.bad:
+            raise RuntimeError("simulated: hipIpcGetMemHandle failed")
+        return bytes([self.rank]) * 64
+
+    def slab_link_import(self, handle):
+        self.imported = handle
+
+
+def _link_worker(rank, world, port, bad, out_path):
+    import time
+    import torch.distributed as dist
+    from globalign_amd import distributed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        links = distributed.Links(dist, rank, world)
+        eng = _LinkOnlyEngine(rank, bad)
+        t0 = time.monotonic()
+        ok = distributed.ipc_agreed(dist, links, eng)
+        np.savez(out_path + f".{rank}.npz", ok=ok, dt=time.monotonic() - t0,
+                 imported=eng.imported if eng.imported is not None else b"")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (3, 1), (3, 2)])
+def test_ipc_export_failure_reaches_the_agreement(world, bad, tmp_path):
+    """a rank whose slab_link_export raises still sends its left neighbour a (None) handle, so the
+    neighbour does not wait out the process group's timeout; every rank reaches the all-reduce at once and
+    agrees on bands.  Ranks whose own links worked have imported their right neighbour's handle."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "link")
+    mp.start_processes(_link_worker, args=(world, _free_port(), bad, out), nprocs=world, join=True, start_method="fork")
+    for r in range(world):
+        res = np.load(out + f".{r}.npz")
+        assert not bool(res["ok"])
+        assert float(res["dt"]) < 20.0
+        if r < world - 1 and bad not in (r, r + 1):
+            assert bytes(res["imported"]) == bytes([r + 1]) * 64

@@ -35,7 +35,8 @@ def _scoring(seq_1, seq_2):
     return cmat, goc
 
 
-def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True, fail_import=False):
+def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True, fail_import=False,
+            fail_export=False):
     import torch
     import torch.distributed as dist
     from globalign_amd import distributed
@@ -52,11 +53,15 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback
             def refuse(handle):
                 raise RuntimeError("simulated: the right neighbour's IPC handle does not open")
             eng.slab_link_import = refuse
+        if fail_export and rank == world - 1:
+            def no_handle():
+                raise RuntimeError("simulated: hipIpcGetMemHandle fails on this rank")
+            eng.slab_link_export = no_handle
         for _ in range(2):  # the second run reuses the context (buffers, progress words)
             res = distributed.align_slabs(dist, links, eng, seq_1, seq_2, tables.codes(seq_1),
                                           tables.codes(seq_2), tables, mt_words, band=band, torch=torch,
                                           traceback=traceback)
-        if fail_import:
+        if fail_import or fail_export:
             assert links.ipc_ok is False  # every rank fell back to bands
         if rank == 0:
             cost, strings, status, mt_after = res
@@ -125,8 +130,9 @@ def _slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
 
 @pytest.mark.parametrize("td", [1, 2])
 def test_gpu_slabs_score_only_diag_match_oracle(td, monkeypatch, tmp_path):
-    """The anti-diagonal fill (chosen automatically for the tall N = 8 slabs of C4) in slab mode: the left
-    edge from the neighbour rank's progress word, the right edge out to it, the cost from the last rank."""
+    """The anti-diagonal fill (GA_FILL_MODE=diag; no longer chosen automatically) in slab mode:
+    the left edge from the neighbour rank's progress word, the right edge out to it, the cost from the last
+    rank."""
     monkeypatch.setenv("GA_FILL_MODE", "diag")
     monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
     _slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
@@ -190,16 +196,19 @@ def test_linked_slabs_abort_propagates(monkeypatch):
     _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
     tables = _native.CostTables(cmat, goc)
     a, b = tables.codes(s1), tables.codes(s2)
-    engines = [distributed.GpuSlabEngine(0) for _ in range(3)]
+    # GA_* knobs are read when a context is created: only the middle slab's context gets the short halo bound
+    engines = [distributed.GpuSlabEngine(0)]
+    monkeypatch.setenv("GA_HALO_SPIN_LIMIT", str(1 << 16))
+    engines.append(distributed.GpuSlabEngine(0))
+    monkeypatch.delenv("GA_HALO_SPIN_LIMIT")
+    engines.append(distributed.GpuSlabEngine(0))
     try:
         edges = distributed.slab_bounds(n, 3)
         for k, eng in enumerate(engines):
             eng.load_slab(a, b, tables, edges[k], edges[k + 1])
         engines[0].slab_link(engines[1])
         engines[1].slab_link(engines[2])
-        monkeypatch.setenv("GA_HALO_SPIN_LIMIT", str(1 << 16))
         engines[1].slab_launch(traceback=False)
-        monkeypatch.delenv("GA_HALO_SPIN_LIMIT")
         t0 = time.monotonic()
         engines[2].slab_launch(traceback=False)
         with pytest.raises(_native.EngineError):
@@ -234,6 +243,26 @@ def test_gpu_slabs_ipc_failure_falls_back_to_bands(tmp_path):
     out = str(tmp_path / "res_fb.npz")
     mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, 600, out, True, True), nprocs=world,
                        join=True, start_method="spawn")
+    r = np.load(out)
+    cmat, goc = _scoring(seq_1, seq_2)
+    ref = core.align(seq_1, seq_2, cmat, goc, mt_words)
+    assert int(r["cost"]) == ref["cost"]
+    assert (str(r["a"]), str(r["mid"]), str(r["b"])) == tuple(ref["strings"])
+    assert r["mt"].tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+
+
+def test_gpu_slabs_ipc_export_failure_falls_back_to_bands(tmp_path):
+    """the last rank's export fails; it still sends its neighbour a (None) handle, every rank agrees on
+    bands at once (no wait for the process group's timeout), and the results stay exact."""
+    import torch.multiprocessing as mp
+    from oracle import core
+    m, n, seed, world = 2400, 4500, 73, 3
+    seq_1, seq_2 = splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna")
+    random.seed(seed)
+    mt_words = np.array(random.getstate()[1], dtype=np.uint32)
+    out = str(tmp_path / "res_fe.npz")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, 600, out, True, False, True),
+                       nprocs=world, join=True, start_method="spawn")
     r = np.load(out)
     cmat, goc = _scoring(seq_1, seq_2)
     ref = core.align(seq_1, seq_2, cmat, goc, mt_words)

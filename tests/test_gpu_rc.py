@@ -136,3 +136,49 @@ def test_rc_worker_lds_caps_stripe_width(monkeypatch):
     kind = _align(monkeypatch, splitmix_seq(3000, 31, "dna"), splitmix_seq(3100, 32, "dna"), DNA, seed=5,
                   env={"GA_LANE_COLS_PER_LANE": 8, "GA_RC_EVERY": 256})
     assert kind[1] == 4, kind
+
+
+def test_rc_streamed_decode_check(monkeypatch):
+    """The streamed level decode under its own detector: GA_RC_DECODE_CHECK records every level
+    word as the host decodes it and fails the call if one changes afterwards (a block published before its
+    stores landed); GA_RC_DECODE_LAG=1 holds the decode one 512-dispatch block behind the progress word."""
+    _align(monkeypatch, splitmix_seq(4000, 91, "dna"), splitmix_seq(4000, 92, "dna"), DNA, seed=91,
+           env={"GA_RC_DECODE_CHECK": 1, "GA_RC_DECODE_LAG": 1})
+    _align(monkeypatch, splitmix_seq(4000, 93, "dna"), splitmix_seq(4000, 94, "dna"), DNA, seed=93,
+           env={"GA_RC_DECODE_CHECK": 1})
+
+
+@pytest.mark.parametrize("servers", [3, 200])
+def test_rc_deep_window_many_block_rows(monkeypatch, servers):
+    """4 columns per lane (blocks of 4 tiles) over ~190 block rows with the full 16 x 16-candidate
+    window, so workers with stale views of the walker race to claim and write blocks 15 rows apart; the 32-deep
+    cache and the write-time reach check must keep every block the walker reads its own."""
+    _align(monkeypatch, splitmix_seq(12000, 95, "dna"), splitmix_seq(3300, 96, "dna"), DNA, seed=servers,
+           env={"GA_LANE_COLS_PER_LANE": 4, "GA_RC_SERVERS": servers, "GA_RC_WIN": 64})
+
+
+def test_rc_checkpoints_over_budget_fall_back(monkeypatch):
+    """Checkpoints that do not fit the budget / the free device memory (GA_RC_BUDGET_MB=0 here) make
+    ga_problem_align take another traceback path instead of failing; the result stays exact."""
+    from globalign_amd import _native
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    s1, s2 = splitmix_seq(2100, 97, "dna"), splitmix_seq(2300, 98, "dna")
+    a1, a2, smat, cmat, gos, goc = transform.settings(dict(DNA, seq_1=s1, seq_2=s2))
+    random.seed(4)
+    mt = np.array(random.getstate()[1], dtype=np.uint32)
+    ref = core.align(a1, a2, cmat, goc, mt)
+    _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **DNA)
+    tables = _native.CostTables(cmat2, goc2)
+    monkeypatch.setenv("GA_RC", "1")
+    monkeypatch.setenv("GA_RC_BUDGET_MB", "0")
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(a1), tables.codes(a2), tables)
+        cost, strings, status, mt_after = eng.align(mt, a1, a2)
+        kind = eng.fill_kind()
+    finally:
+        eng.close()
+    assert kind[0] != "rc", kind
+    assert status == 0 and int(cost) == ref["cost"] and tuple(strings) == tuple(ref["strings"])
+    assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
