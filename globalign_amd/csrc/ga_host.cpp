@@ -721,7 +721,12 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
             else
                 for (every = 64; every < 4096 && !fits(every); every *= 2) {}
             if (1024 + ga::rc_worker_bytes(c->T, c->CB, every) <= kRcLds) break;
-            if (c->T == 1) return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
+            if (c->T == 1) {
+                // no spacing fits both: memory if the densest one fits LDS, else LDS
+                if (1024 + ga::rc_worker_bytes(1, c->CB, 64) <= kRcLds)
+                    return fail(GA_E_NOMEM, "recompute walk: the checkpoints do not fit the budget / free device memory");
+                return fail(GA_E_RANGE, "recompute walk: a block's codes do not fit LDS");
+            }
             if (!lane_geometry(c, n, &qrows, false, c->T / 2, 4)) return fail(GA_E_STATE, "recompute fill geometry");
         }
         if (ck_bytes(every) > std::min(budget, dev_avail - other_bytes()))
@@ -812,6 +817,10 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.lane_sub = e ? atoi(e) : -1;
         e = c->knob("GA_LANE_TB_SUB");
         p.lane_tb_sub = e ? atoi(e) : -1;
+        e = c->knob("GA_LANE_ASM");
+        p.asm_step = e ? atoi(e) : 1;
+        e = c->knob("GA_LANE_IOPRIO");
+        p.io_prio = e ? atoi(e) : 0;
     }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);

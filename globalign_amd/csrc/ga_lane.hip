@@ -29,6 +29,7 @@
 
 #include "ga_device.h"
 #include "ga_lane.h"
+#include "ga_lane_asm.h"
 #include "ga_sync.h"
 
 #ifndef GA_LANE_LE
@@ -38,7 +39,7 @@
 namespace ga {
 
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
-    return (size_t)LK_CNT_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + LK_QMIRROR) * 4 +
+    return (size_t)LK_HEAD_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + LK_QMIRROR) * 4 +
            (size_t)K * 32;  // + the K x K int8 sub' table (K <= 32)
 }
 
@@ -58,10 +59,10 @@ size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
 // more cycles per step): for one-round chains (C3, slabs), whose time is m steps plus every stripe's lag;
 // fills in rounds (C4 on one GPU) run uncoupled and keep the early reads
 template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false, bool RC = false, bool LATE = false>
-__global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
+__global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
-    int2* ring = reinterpret_cast<int2*>(smem + LK_CNT_BYTES);
+    int2* ring = reinterpret_cast<int2*>(smem + LK_HEAD_BYTES);
     uint32_t* pq = reinterpret_cast<uint32_t*>(ring + (NWC + 1) * RING);
     const int QR = p.qrows;  // profile ring rows (power of two)
     const int QS = QR + LK_QMIRROR;
@@ -72,6 +73,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    if (threadIdx.x < 32) reinterpret_cast<unsigned*>(smem + LK_ZERO_OFF)[threadIdx.x] = 0u;  // the zero block
     for (int q = threadIdx.x; q < K * K; q += blockDim.x) stab[(q / K) * 32 + q % K] = (int8_t)p.subp[q];
     __syncthreads();
     if (threadIdx.x == 0) cnt[LK_SLAB] = atomicAdd(p.ticket, 1u);
@@ -85,8 +87,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     const int nwin = CB > 0 ? tca + 4 : (nsteps + 15) / 16;
     const int nlive = min(NWC, p.nstripes - g * NWC);
 
+    // the IO and profile waves share SIMDs with compute waves (priority 2): at a lower priority they issue only
+    // when their compute wave stalls, which delays hand-offs and profile rows (GA_LANE_IOPRIO, experiments)
+    auto io_prio = [&]() {
+        if (p.io_prio >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (p.io_prio == 2) __builtin_amdgcn_s_setprio(2);
+        else if (p.io_prio == 1) __builtin_amdgcn_s_setprio(1);
+    };
     if (w == NWC) {
-        // ---------------- IO wave: edges HBM <-> LDS rings, the profile table ----------------
+        // ---------------- IO wave: edges HBM <-> LDS rings ----------------
+        io_prio();
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
         const unsigned* src_prog = g == 0 ? p.left_prog : nullptr;
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
@@ -96,43 +106,9 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         int2* rin0 = ring;
         const int2* rout = ring + nlive * RING;
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
-        unsigned in_next = 0, out_next = 0, q_next = 0, spins = 0, in_win = 64;
-        // dword row r of code c: sub'(a_r .. a_r+3, c), rows outside 1..m zero.  A lane's window
-        // may start up to 3 rows above row 1 (its first sub-chunk), so rows -2..0 are written too.
-        auto put_dword = [&](int r) {
-            int x[4];
-            bool ok[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                ok[u] = r + u >= 1 && r + u <= m;
-                x[u] = ok[u] ? p.a[r + u - 1] : 0;
-            }
-            const unsigned slot = (unsigned)(r - 1) & qmask;
-            for (int c = 0; c < K; c++) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int u = 0; u < 4; u++) v |= ok[u] ? (uint32_t)(uint8_t)stab[x[u] * 32 + c] << (8 * u) : 0u;
-                pq[c * QS + slot] = v;
-                if (slot < (unsigned)LK_QMIRROR) pq[c * QS + QR + slot] = v;
-            }
-        };
-        if (lane < 3) put_dword(lane - 2);
-        while (in_next < (unsigned)m || out_next < (unsigned)m || q_next < (unsigned)m) {
+        unsigned in_next = 0, out_next = 0, spins = 0, in_win = 64;
+        while (in_next < (unsigned)m || out_next < (unsigned)m) {
             bool moved = false;
-            if (q_next < (unsigned)m) {
-                // the slowest wave reads rows above (its output rows) - 16, so slots of rows below
-                // that + QR are free
-                const unsigned pl = lds_ld(&cnt[2 * nlive - 1]);
-                const unsigned space = (pl > 32u ? pl - 32u : 0u) + (unsigned)QR;
-                const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
-                if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
-                    const unsigned r = q_next + 1 + lane;
-                    if (r <= hi) put_dword((int)r);
-                    if (lane == 0) lds_st(&cnt[LK_PRODQ], hi == (unsigned)m ? LK_DONE : hi);
-                    q_next = hi;
-                    moved = true;
-                }
-            }
             if (in_next < (unsigned)m && in_sent) {
                 const unsigned cap = min(min(lds_ld(&cnt[0]) + RING, (unsigned)m), in_next + in_win);
                 if (cap > in_next) {
@@ -215,6 +191,54 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
         if (!out_sent && out_next < (unsigned)m && p.edge_prog != nullptr && lane == 0) s_prog_abort(p.edge_prog);
         return;
     }
+    if (w == NWC + 1) {
+        // ---------------- profile wave: the LDS query-profile table, ahead of the slowest compute wave.  A wave
+        // of its own (round 3: the IO wave's), so that the hand-off rows never wait behind it: for a 24-code
+        // alphabet the table's 64-row batches held the IO wave long enough to triple the cross-workgroup lag
+        // (28 us against 8.5 for DNA, profiles/r03/lane_stamps_c5_shape.jsonl)
+        io_prio();
+        // dword row r of code c: sub'(a_r .. a_r+3, c), rows outside 1..m zero.  A lane's window
+        // may start up to 3 rows above row 1 (its first sub-chunk), so rows -2..0 are written too.
+        auto put_dword = [&](int r) {
+            int x[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                ok[u] = r + u >= 1 && r + u <= m;
+                x[u] = ok[u] ? p.a[r + u - 1] : 0;
+            }
+            const unsigned slot = (unsigned)(r - 1) & qmask;
+            for (int c = 0; c < K; c++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int u = 0; u < 4; u++) v |= ok[u] ? (uint32_t)(uint8_t)stab[x[u] * 32 + c] << (8 * u) : 0u;
+                pq[c * QS + slot] = v;
+                if (slot < (unsigned)LK_QMIRROR) pq[c * QS + QR + slot] = v;
+            }
+        };
+        if (lane < 3) put_dword(lane - 2);
+        unsigned q_next = 0, spins = 0;
+        while (q_next < (unsigned)m) {
+            // the slowest wave reads rows above (its output rows) - 16, so slots of rows below that + QR are free
+            const unsigned pl = lds_ld(&cnt[2 * nlive - 1]);
+            const unsigned space = (pl > 32u ? pl - 32u : 0u) + (unsigned)QR;
+            const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
+            if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
+                const unsigned r = q_next + 1 + lane;
+                if (r <= hi) put_dword((int)r);
+                if (lane == 0) lds_st(&cnt[LK_PRODQ], hi == (unsigned)m ? LK_DONE : hi);
+                q_next = hi;
+                spins = 0;
+            } else {
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) break;
+                if (!spin_ok(spins, p.spin_limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
+            }
+        }
+        return;
+    }
     if (w >= nlive) return;
 
     // ---------------- compute wave w: stripe s, columns j0+1 .. j0+64*TD ----------------
@@ -259,6 +283,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     int Hl = H[TD - 1], Xl = 0, RH = 0, RX = 0;
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
+    // the hand-scheduled asm step (ga_lane_asm.h) for the unmasked sub-chunks of the score-only fills
+    constexpr bool ASMOK = CB == 0 && !CKP && SUB == 16;
+    const bool use_asm = ASMOK && p.asm_step;
+    // asm sub-chunks keep lane 63's rows in registers (no DPP shift registers): the RC right-edge checkpoints
+    // and the direct hand-off read them back from the output ring (lanes 0..15) and store them one sub-chunk
+    // later, when the read has long landed
+    int2 pend_v = make_int2(0, 0);
+    int pend_row = 0;
     unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
     // the workgroup's last compute wave writes the hand-off rows (not a slab's halo to another GPU, which
     // the IO wave streams with its progress word)
@@ -266,6 +298,19 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     const bool hand_direct = p.hand_direct && w == nlive - 1 && !(last_slab_w && p.edge_out != nullptr);
     int2* hand_out = p.hand + (long long)g * (m + 1);
     const bool last_full = last_slab_w && p.n % (64 * TD) == 0;
+    auto flush_pend = [&]() {
+        if (ASMOK && pend_row > 0) {
+            const int row = pend_row + lane;
+            if (lane < SUB && row >= 1 && row <= m) {
+                if (RC && p.colck != nullptr) p.colck[(long long)s * (m + 1) + row] = pend_v;
+                if (hand_direct) {
+                    g_st64(hand_out + row, pend_v);
+                    if (row == m && last_full) p.out_last[0] = pend_v.x;  // H'(m, n): the cost
+                }
+            }
+            pend_row = 0;
+        }
+    };
     unsigned* cons_out = &cnt[2 * w + 2];
     unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
@@ -295,8 +340,14 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
     int4 A[NE], B[NE];
     uint32_t qA[TD][NQ], qB[TD][NQ];
     wait_ge(prod_in, 0, avail, SUB, 0);
+    // the edge rows: lane 0 reads them from the ring, lanes 1..63 read the zero block (the asm step adds the
+    // edge register to the zero-filled DPP shift; the compiler's step takes lane 0's value only)
+    const int4* const ezero = reinterpret_cast<const int4*>(smem + LK_ZERO_OFF);
+    {
+        const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin) : ezero;
 #pragma unroll
-    for (int k = 0; k < NE; k++) A[k] = reinterpret_cast<const int4*>(rin)[k];
+        for (int k = 0; k < NE; k++) A[k] = src[k];
+    }
     wait_ge(&cnt[LK_PRODQ], 0, qavail, SUB, 1);
     {
         const unsigned idx = (unsigned)(-lane) & qmask;
@@ -350,8 +401,11 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 avail = sgpr_u(max(avail, pnext));
                 if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
             }
+            {
+                const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK)) : ezero;
 #pragma unroll
-            for (int k = 0; k < NE; k++) Nx[k] = reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK))[k];
+                for (int k = 0; k < NE; k++) Nx[k] = src[k];
+            }
             pnext = __hip_atomic_load(prod_in, RLX, WGS);
             asm volatile("" ::: "memory");
         };
@@ -388,6 +442,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             };
             one(std::integral_constant<int, 0>{});
             qloads();
+            flush_pend();
             if constexpr (LE > 0) {
                 LkUnroll<1, LE>::run(one);
                 eloads();
@@ -412,7 +467,60 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
                 steps(std::false_type{}, std::false_type{});
             }
         } else {
-            if (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB) steps(std::true_type{}, std::false_type{});
+            const bool masked = r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB;
+            if constexpr (ASMOK) {
+                if (use_asm && !masked) {
+                    // lane 63's rows of this sub-chunk stay in registers (the asm step's hn / ex)
+                    int oh[SUB], ox[SUB];
+                    // steps 4d+u0 .. 4d+u0+n-1 (profile dwords d) in one asm statement
+                    auto blk = [&](auto D, auto U0, auto N) {
+                        constexpr int d = decltype(D)::value, u0 = decltype(U0)::value, n = decltype(N)::value;
+                        constexpr int u = 4 * d + u0;
+                        uint32_t qq[TD];
+#pragma unroll
+                        for (int k = 0; k < TD; k++) qq[k] = qc[k][d];
+                        LaneAsm<TD, u0, n>::run(H, Y, Xl, HLp, eh + u, ex + u, qq, o, oh + u, ox + u);
+                    };
+                    using I0 = std::integral_constant<int, 0>;
+                    using I1 = std::integral_constant<int, 1>;
+                    using I2 = std::integral_constant<int, 2>;
+                    using I3 = std::integral_constant<int, 3>;
+                    using I4 = std::integral_constant<int, 4>;
+                    static_assert(LE == 0 || LE == 13, "asm sub-chunk layout");
+                    if constexpr (LE == 13) {
+                        blk(I0{}, I0{}, I4{});
+                        qloads();
+                        flush_pend();
+                        blk(I1{}, I0{}, I4{});
+                        blk(I2{}, I0{}, I4{});
+                        blk(I3{}, I0{}, I1{});
+                        eloads();
+                        blk(I3{}, I1{}, I3{});
+                    } else {
+                        blk(I0{}, I0{}, I1{});
+                        qloads();
+                        eloads();
+                        flush_pend();
+                        blk(I0{}, I1{}, I3{});
+                        blk(I1{}, I0{}, I4{});
+                        blk(I2{}, I0{}, I4{});
+                        blk(I3{}, I0{}, I4{});
+                    }
+                    Hl = H[TD - 1];
+                    const int rlo = r0 - 62;
+                    if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
+                    const unsigned b1 = rout_lds + (unsigned)((rlo - 1) & RMASK) * 8u;
+                    const unsigned b2 = rout_lds + (unsigned)((rlo - 1 + SUB - 1) & RMASK) * 8u;
+                    const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
+                    lk_store_rows(b1, b2, pc_lds, cp, oh, ox);
+                    if ((RC && p.colck != nullptr) || hand_direct) {
+                        pend_row = rlo;
+                        pend_v = rout[(rlo - 1 + (lane & (SUB - 1))) & RMASK];
+                    }
+                    return;
+                }
+            }
+            if (masked) steps(std::true_type{}, std::false_type{});
             else steps(std::false_type{}, std::false_type{});
         }
         // lane 63 computed rows r0-62 .. r0-63+SUB; lanes 64-SUB..63 of the shift registers hold them
@@ -503,6 +611,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) fill_lane_kernel(FillArgs p) {
             }
         }
     }
+    flush_pend();  // the last asm sub-chunk's read-back rows
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
     if (partial && lane == cn / TD) p.out_last[0] = Hm;
@@ -534,7 +643,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.stck != nullptr) {
             auto* fc = fill_lane_kernel<NWC, TD, 0, 16, false, false, true, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
             return;
         }
     }
@@ -542,7 +651,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.ckpt != nullptr) {  // 8-step sub-chunks: with 16 the checkpoint stores spill at TD >= 4
             auto* fc = fill_lane_kernel<NWC, TD, CB, 8, false, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
             return;
         }
     }
@@ -550,13 +659,13 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.late) {
             auto* fl = fill_lane_kernel<NWC, TD, 0, 16, DBG, false, false, true>;
             (void)hipFuncSetAttribute((const void*)fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fl<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+            fl<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
             return;
         }
     }
     auto* fn = fill_lane_kernel<NWC, TD, CB, SUB, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 1)), lds, s>>>(p);
+    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
 }
 
 // variants without spills (vgpr_spill_count of the code object; lane_geometry keeps to them): score
