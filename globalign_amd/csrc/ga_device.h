@@ -54,6 +54,7 @@ struct FillArgs {
     int lds_floor, lane_sub, lane_tb_sub;
     int asm_step;             // lane fill, score only: the hand-scheduled asm step (ga_lane_asm.h; GA_LANE_ASM)
     int io_prio;              // lane fill: s_setprio of the IO and profile waves (GA_LANE_IOPRIO; 0: none)
+    int fine;                 // lane fill, asm sub-chunks: edges awaited and published per 4-step block (GA_LANE_FINE)
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),

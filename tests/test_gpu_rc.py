@@ -60,6 +60,15 @@ def test_rc_stripe_widths_vs_oracle(monkeypatch, td):
     assert kind[1] == td
 
 
+@pytest.mark.parametrize("env", [{"GA_LANE_FINE": 0}, {"GA_LANE_DIRECT": 1}, {"GA_LANE_DIRECT": 1, "GA_LANE_FINE": 0},
+                                 {"GA_LANE_ASM": 0}])
+def test_rc_handover_variants_vs_oracle(monkeypatch, env):
+    """The checkpointing fill under each edge hand-over: the right-edge checkpoints are read back
+    from the output ring whether lane 63's rows went out per 4-step block or per sub-chunk."""
+    _align(monkeypatch, splitmix_seq(3100, 51, "dna"), splitmix_seq(64 * 2 * 4 * 5 + 77, 52, "dna"), DNA, seed=3,
+           env=dict(env, GA_LANE_COLS_PER_LANE=2))
+
+
 @pytest.mark.parametrize("every", [128, 256])
 def test_rc_checkpoint_spacing_vs_oracle(monkeypatch, every):
     """Sparser staircase checkpoints: a block is recomputed from up to every + 126 steps above it."""
