@@ -821,8 +821,6 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.asm_step = e ? atoi(e) : 1;
         e = c->knob("GA_LANE_IOPRIO");
         p.io_prio = e ? atoi(e) : 0;
-        e = c->knob("GA_LANE_FINE");
-        p.fine = e ? atoi(e) : 0;  // measured slower so far (tools/micro/lane_fine.hip)
     }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);

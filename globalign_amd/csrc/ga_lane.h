@@ -13,12 +13,12 @@ namespace ga {
 // [LK_PROD0] (ring 0, the IO wave's), so compute wave w publishes {cons(w), prod(w+1)} in one store
 enum { LK_PROD0 = 31, LK_PRODQ = 40, LK_ABORT = 41, LK_SLAB = 42 };
 constexpr int LK_CNT_BYTES = 256;
-// after the counters: a zero block that lanes 1..63 read as their "edge" rows, so that a step can add its edge
-// register to a zero-filled DPP shift (ga_lane_asm.h): a ring's rows and a block more, so that lane 0's ring slot
-// offset also addresses zeros in it (the fine hand-over reads both with one address add); the rings start after it
+// after the counters: a zero block (16 rows of int2) that lanes 1..63 read as their "edge" rows, so that a step
+// can add its edge register to a zero-filled DPP shift (ga_lane_asm.h); then a scratch slot of 8 bytes per lane for
+// the lean sub-chunk's all-lane row stores (lanes that carry no row write there); the rings start after it
 constexpr int LK_ZERO_OFF = LK_CNT_BYTES;
-constexpr int LK_ZERO_BYTES = 256 * 8 + 16 * 8;
-constexpr int LK_HEAD_BYTES = LK_ZERO_OFF + LK_ZERO_BYTES;
+constexpr int LK_SCR_OFF = LK_ZERO_OFF + 16 * 8;
+constexpr int LK_HEAD_BYTES = LK_SCR_OFF + 64 * 8;
 constexpr int LK_QMIRROR = 16;  // profile slots mirrored past the ring's end (a window reads idx .. idx+12)
 constexpr unsigned LK_DONE = 0x7fffffffu;
 typedef unsigned lk_v2u __attribute__((ext_vector_type(2)));

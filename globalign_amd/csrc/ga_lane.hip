@@ -73,8 +73,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
-    for (int q = threadIdx.x; q < LK_ZERO_BYTES / 4; q += blockDim.x)
-        reinterpret_cast<unsigned*>(smem + LK_ZERO_OFF)[q] = 0u;  // the zero block
+    if (threadIdx.x < 32) reinterpret_cast<unsigned*>(smem + LK_ZERO_OFF)[threadIdx.x] = 0u;  // the zero block
     for (int q = threadIdx.x; q < K * K; q += blockDim.x) stab[(q / K) * 32 + q % K] = (int8_t)p.subp[q];
     __syncthreads();
     if (threadIdx.x == 0) cnt[LK_SLAB] = atomicAdd(p.ticket, 1u);
@@ -285,14 +284,16 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
     // the hand-scheduled asm step (ga_lane_asm.h) for the unmasked sub-chunks of the score-only fills
-    constexpr bool ASMOK = CB == 0 && !CKP && SUB == 16;
+    // (not at 8 waves per workgroup with TD >= 4: the register budget of 640-thread workgroups cannot hold the
+    // lean sub-chunk, and register allocation then runs for tens of minutes)
+    constexpr bool ASMOK = CB == 0 && !CKP && SUB == 16 && (NWC == 4 || TD <= 2);
     const bool use_asm = ASMOK && p.asm_step;
     // asm sub-chunks keep lane 63's rows in registers (no DPP shift registers): the RC right-edge checkpoints
     // and the direct hand-off read them back from the output ring (lanes 0..15) and store them one sub-chunk
     // later, when the read has long landed
     int2 pend_v = make_int2(0, 0);
     int pend_row = 0;
-    bool pend_hand = false;  // the pending rows still go to the hand-off (the fine path stores them per block)
+    bool pend_hand = false;  // the pending rows (GA_LANE_ASM=2 sub-chunks) also go to the hand-off rows
     unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
     // the workgroup's last compute wave writes the hand-off rows (not a slab's halo to another GPU, which
     // the IO wave streams with its progress word)
@@ -345,10 +346,11 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     // the edge rows: lane 0 reads them from the ring, lanes 1..63 read the zero block (the asm step adds the
     // edge register to the zero-filled DPP shift; the compiler's step takes lane 0's value only)
     const int4* const ezero = reinterpret_cast<const int4*>(smem + LK_ZERO_OFF);
-    // the fine hand-over's read addresses: lane 0 its input ring, lanes 1..63 the zero block (a ring's size, so the
-    // same slot offset stays inside it); the producer's counter
-    const unsigned ebase = lane == 0 ? lds_addr(rin) : lds_addr(ezero);
+    // the lean sub-chunk's LDS addresses: the producer's counter, the profile table, a scratch slot per lane (the
+    // all-lane row stores of lanes that carry no row)
     const unsigned ca_lds = lds_addr(prod_in);
+    const unsigned pq_lds = lds_addr(pq);
+    const unsigned scr_lds = lds_addr(smem + LK_SCR_OFF);
     {
         const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin) : ezero;
 #pragma unroll
@@ -475,91 +477,72 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         } else {
             const bool masked = r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB;
             if constexpr (ASMOK) {
-                if (use_asm && !masked && p.fine) {
-                    // Fine-grained hand-over: the edges are awaited and the outputs published per
-                    // 4-step block instead of per sub-chunk.  After a block's first step the wave reads the
-                    // producer's counter and then, without waiting for it, the next block's four edge rows (one asm
-                    // statement with the block's steps, LaneBlk); LDS executes a wave's operations in order and the
-                    // producer writes its rows before its counter, so a counter that covers the rows proves the rows
-                    // read after it.  It is checked after the block's last step (the reads have long landed); only
-                    // a producer that really is behind sends the wave to a poll and a re-read.  Lane 63's four rows
-                    // then go out with the counters.  A stripe trails its left neighbour by ~64 + 8 steps instead of
-                    // 64 + 16 + the read-ahead.
+                if (use_asm && !masked && p.asm_step == 1) {
+                    // The lean sub-chunk: the 16 steps, the next sub-chunk's profile and edge reads
+                    // and lane 63's rows out as ONE asm statement (LaneSub, ga_lane_asm.h), so that no compiler code,
+                    // copy or conservative wait sits between the steps.  Lane 63's rows go out by DPP moves into
+                    // lanes 48..63 and two all-lane ds_write2_b32 (1 + 2 LDS writes instead of 17); the producer's
+                    // counter is read just before the edge rows, so a counter that covers them proves them (LDS
+                    // executes a wave's operations in order, the producer writes rows before its counter) and only a
+                    // producer that really is behind costs a poll and a re-read.
                     const int rlo = r0 - 62;
                     if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
-                    qloads();
-                    flush_pend();
-                    // the sub-chunk's 16 output slots start at 1 mod 16: only its last row can wrap
-                    const unsigned b1 = rout_lds + (unsigned)((rlo - 1) & RMASK) * 8u;
-                    const unsigned b2 = rout_lds + (unsigned)((rlo - 1 + SUB - 1) & RMASK) * 8u;
-                    lk_v4i E0 = {C[0].x, C[0].y, C[0].z, C[0].w}, E1 = {C[1].x, C[1].y, C[1].z, C[1].w};
-                    auto fblk = [&](auto D) {
-                        constexpr int d = decltype(D)::value;
-                        const int eh4[4] = {E0.x, E0.z, E1.x, E1.z}, ex4[4] = {E0.y, E0.w, E1.y, E1.w};
-                        uint32_t qq[TD];
+                    lk_v4i Ev[NE];
 #pragma unroll
-                        for (int k = 0; k < TD; k++) qq[k] = qc[k][d];
-                        // rows nr+1 .. nr+4 (ring slots nr .. nr+3, a 4-aligned run: never wraps); lanes 1..63 read
-                        // the zero block at the same offset
-                        const int nr = r0 + 4 * d + 4;
-                        unsigned cv;
-                        lk_v4i N0, N1;
-                        int h4[4], x4[4];
-                        LaneBlk<TD>::run(H, Y, Xl, HLp, eh4, ex4, qq, o, h4, x4, ca_lds, ebase + (unsigned)(nr & RMASK) * 8u,
-                                         cv, N0, N1);
-                        const int need = min(nr + 4, m);
-                        if ((int)sgpr_u(cv) < need) {
-                            wait_ge(prod_in, 0, avail, need, 0);
-                            asm volatile("" ::: "memory");
-                            const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin + (nr & RMASK)) : ezero;
-                            const int4 n0 = src[0], n1 = src[1];
-                            N0 = lk_v4i{n0.x, n0.y, n0.z, n0.w};
-                            N1 = lk_v4i{n1.x, n1.y, n1.z, n1.w};
-                            // landed before the publish's LDS writes (which the compiler does not count)
-                            asm volatile("" ::"v"(N0), "v"(N1) : "memory");
-                        }
-                        lk_store_rows4<d>(b1, b2, pc_lds, lk_v2u{(unsigned)(nr + 4), (unsigned)max(rlo + 4 * d + 3, 0)},
-                                          h4, x4);
-                        if (hand_direct) {
-                            // the workgroup's right edge straight to its hand-off rows, four at a time (agent-scope
-                            // 8-byte stores: each row one untorn granule the next workgroup's IO wave polls for)
-                            const int row0 = rlo + 4 * d;
-                            if (lane == 63) {
+                    for (int k = 0; k < NE; k++) Ev[k] = lk_v4i{C[k].x, C[k].y, C[k].z, C[k].w};
+                    const unsigned ea = lane == 0 ? lds_addr(rin + ((r0 + SUB) & RMASK)) : lds_addr(ezero);
+                    const unsigned qi = (unsigned)(r0 + SUB - lane) & qmask;
+                    unsigned qbv[TD];
 #pragma unroll
-                                for (int u = 0; u < 4; u++)
-                                    if (row0 + u >= 1 && row0 + u <= m) g_st64(hand_out + row0 + u, make_int2(h4[u], x4[u]));
-                                if (last_full && row0 <= m && m < row0 + 4) p.out_last[0] = h4[m - row0];
-                            }
-                        }
-                        E0 = N0;
-                        E1 = N1;
-                    };
-                    fblk(std::integral_constant<int, 0>{});
-                    fblk(std::integral_constant<int, 1>{});
-                    fblk(std::integral_constant<int, 2>{});
-                    fblk(std::integral_constant<int, 3>{});
+                    for (int k = 0; k < TD; k++) qbv[k] = pq_lds + 4u * (qb[k] + qi);
+                    const unsigned slot = rout_lds + 8u * ((unsigned)(rlo - 1 + lane - 48) & RMASK);
+                    const unsigned scr = scr_lds + 8u * (unsigned)lane;
+                    const bool hi = lane >= 48;
+                    const unsigned wa = hi && (lane & 4) ? slot : scr, wb = hi && !(lane & 4) ? slot : scr;
+                    const unsigned wc = lane == 0 ? pc_lds : scr;
+                    const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
+                    unsigned cv;
+                    lk_v4i En[NE];
+                    lk_v2u qn[TD][2];
+                    int R[4];
+                    LaneSub<TD, LE ? 12 : 0>::run(H, Y, Xl, HLp, Ev, qc, o, ca_lds, ea, qbv, wa, wb, wc, cp, cv, En, qn, R);
                     Hl = H[TD - 1];
-                    if ((unsigned)(tm - (r0 + SUB)) < (unsigned)SUB) {
-                        // the next sub-chunk is a masked one (a partial stripe's row m): it takes all its rows at once
-                        wait_ge(prod_in, 0, avail, min(r0 + 2 * SUB, m), 0);
+                    const int need = min(r0 + 2 * SUB, m);
+                    if ((int)sgpr_u(cv) < need) {
+                        wait_ge(prod_in, 0, avail, need, 0);
                         asm volatile("" ::: "memory");
                         const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK)) : ezero;
 #pragma unroll
                         for (int k = 0; k < NE; k++) Nx[k] = src[k];
                         asm volatile("" ::: "memory");
                     } else {
-                        Nx[0] = make_int4(E0.x, E0.y, E0.z, E0.w);
-                        Nx[1] = make_int4(E1.x, E1.y, E1.z, E1.w);
+#pragma unroll
+                        for (int k = 0; k < NE; k++) Nx[k] = make_int4(En[k].x, En[k].y, En[k].z, En[k].w);
                     }
-                    if (RC && p.colck != nullptr) {
-                        pend_row = rlo;
-                        pend_hand = false;
-                        pend_v = rout[(rlo - 1 + (lane & (SUB - 1))) & RMASK];
+#pragma unroll
+                    for (int k = 0; k < TD; k++) {
+                        qx[k][0] = qn[k][0].x;
+                        qx[k][1] = qn[k][0].y;
+                        qx[k][2] = qn[k][1].x;
+                        qx[k][3] = qn[k][1].y;
+                    }
+                    if ((RC && p.colck != nullptr) || hand_direct) {
+                        // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge
+                        const int row = rlo + lane - 48;
+                        const int2 v = (lane & 4) ? make_int2(R[0], R[1]) : make_int2(R[2], R[3]);
+                        if (hi && row >= 1 && row <= m) {
+                            if (RC && p.colck != nullptr) p.colck[(long long)s * (m + 1) + row] = v;
+                            if (hand_direct) {
+                                g_st64(hand_out + row, v);
+                                if (row == m && last_full) p.out_last[0] = v.x;  // H'(m, n): the cost
+                            }
+                        }
                     }
                     return;
                 }
                 if (use_asm && !masked) {
-                    // lane 63's rows of this sub-chunk stay in registers (the asm step's hn / ex)
+                    // (GA_LANE_ASM=2) the round-3 asm sub-chunk: lane 63's rows of this sub-chunk stay in registers
+                    // (the asm step's hn / ex)
                     int oh[SUB], ox[SUB];
                     // steps 4d+u0 .. 4d+u0+n-1 (profile dwords d) in one asm statement
                     auto blk = [&](auto D, auto U0, auto N) {
@@ -714,7 +697,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         d[4] = wcyc[2];
         d[5] = __builtin_amdgcn_s_memtime() - c_start;
         d[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID: wave, SIMD, CU, SE
-        d[7] = 0;
+        d[7] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID: the XCD (bits 3:0)
     }
 }
 

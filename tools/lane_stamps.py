@@ -64,6 +64,16 @@ for sd in range(4):
                                                                  (m + 63)))}
 by_wave = {int(w): {"wait_edge_frac": float(np.median(st[wave_in_wg == w, 2] / tot[wave_in_wg == w])),
                     "simd_mode": int(np.bincount(simd[wave_in_wg == w]).argmax())} for w in range(min(nwc, ns))}
+xcc = st[:, 7] & 0xF
+xcross = xcc[1:] != xcc[:-1]
+pct = {f"p{q}": float(np.percentile(elag, q)) for q in (10, 50, 90, 99)} if len(elag) else {}
+top = np.argsort(elag)[::-1][:12] if len(elag) else []
+dist = {"end_lag_pct_us": pct, "end_lag_max_us": float(elag.max()) if len(elag) else None,
+        "end_lag_sum_ms": {"intra": float(elag[~cross].sum() / 1e3), "cross_same_xcd": float(elag[cross & ~xcross].sum() / 1e3),
+                           "cross_other_xcd": float(elag[cross & xcross].sum() / 1e3)},
+        "cross_wg_links": {"same_xcd": int((cross & ~xcross).sum()), "other_xcd": int((cross & xcross).sum())},
+        "end_lag_top": [{"stripe": int(i + 1), "lag_us": float(elag[i]), "wave": int((i + 1) % nwc),
+                         "cross": bool(cross[i]), "xcd": [int(xcc[i]), int(xcc[i + 1])]} for i in top]}
 print(json.dumps({
     "m": m, "n": n, "cost": int(cost), "kind": kind, "TD": T, "nstripes": ns, "nwc": nwc, "nslabs": nslabs,
     "fill_ms_plain": plain_ms, "fill_ms_dbg": eng.kernel_ms()[0],
@@ -77,5 +87,5 @@ print(json.dumps({
     "stripe_dur_us_median": float(np.median(dur)), "stripe_dur_us_max": float(dur.max()),
     "ns_per_step_median": float(np.median(dur) * 1e3 / (m + 63)),
     "cycles_per_step_median": float(np.median(tot / (m + 63))),
-    "by_simd": by_simd, "by_wave": by_wave,
+    "by_simd": by_simd, "by_wave": by_wave, "lag_distribution": dist,
 }), flush=True)

@@ -29,7 +29,7 @@ using namespace ga;
 constexpr int LDSW = 12288;  // ints: [0,4096) profile table, [4096,6144) rings, [6144,8192) zero block, rest scratch
 
 template <int TD, int MODE>
-__global__ void __launch_bounds__(256) bench(long long* out, int* sink, int nsteps, int o, int never) {
+__global__ void __launch_bounds__(512) bench(long long* out, int* sink, int nsteps, int o, int never) {
     __shared__ __attribute__((aligned(16))) int lds[LDSW];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -60,10 +60,10 @@ __global__ void __launch_bounds__(256) bench(long long* out, int* sink, int nste
     for (int k = 0; k < 8; k++) E[k] = make_int4(0, 0, 0, 0);
     int acc = 0, RH = 0, RX = 0;
     unsigned cnt_v = 0;
-    int4* ringw = reinterpret_cast<int4*>(lds + 4096 + 512 * w);
+    int4* ringw = reinterpret_cast<int4*>(lds + 4096 + 512 * (w & 3));
     const int4* zero4 = reinterpret_cast<const int4*>(lds + 6144);
     const unsigned outb = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int*)(lds + 4096 + 512 * ((w + 1) & 3));
-    const unsigned pc = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int*)(lds + 8192 + 16 * w);
+    const unsigned pc = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int*)(lds + 8192 + 16 * (w & 3));
     int ohs[16], oxs[16];
     long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < nsteps; r += 16) {
@@ -117,6 +117,25 @@ __global__ void __launch_bounds__(256) bench(long long* out, int* sink, int nste
                         sqn[0] = pk[0]; sqn[1] = pk[4]; sqn[2] = pk[8]; sqn[3] = pk[12];
                     }
                     if constexpr (CHK || MODE == 8) cnt_v = lds[8192 + 16 * ((w + 3) & 3)];
+                    if constexpr (MODE == 12) {  // edge reads from lane 0 only (exec mask), no zero-block returns
+                        const unsigned ea = (unsigned)(uintptr_t)(__attribute__((address_space(3))) int4*)(ringw + ((r >> 1) & 63));
+                        unsigned long long saved;
+                        typedef int v4i __attribute__((ext_vector_type(4)));
+                        v4i a0, a1, a2, a3, a4, a5, a6, a7;
+                        asm volatile("s_mov_b64 %[sv], exec\n\ts_mov_b64 exec, 1\n\t"
+                                     "ds_read_b128 %[a0], %[ea]\n\tds_read_b128 %[a1], %[ea] offset:16\n\t"
+                                     "ds_read_b128 %[a2], %[ea] offset:32\n\tds_read_b128 %[a3], %[ea] offset:48\n\t"
+                                     "ds_read_b128 %[a4], %[ea] offset:64\n\tds_read_b128 %[a5], %[ea] offset:80\n\t"
+                                     "ds_read_b128 %[a6], %[ea] offset:96\n\tds_read_b128 %[a7], %[ea] offset:112\n\t"
+                                     "s_mov_b64 exec, %[sv]\n\ts_waitcnt lgkmcnt(0)"
+                                     : [sv] "=&s"(saved), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+                                       [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7)
+                                     : [ea] "v"(ea) : "memory");
+                        En[0] = make_int4(a0.x, a0.y, a0.z, a0.w); En[1] = make_int4(a1.x, a1.y, a1.z, a1.w);
+                        En[2] = make_int4(a2.x, a2.y, a2.z, a2.w); En[3] = make_int4(a3.x, a3.y, a3.z, a3.w);
+                        En[4] = make_int4(a4.x, a4.y, a4.z, a4.w); En[5] = make_int4(a5.x, a5.y, a5.z, a5.w);
+                        En[6] = make_int4(a6.x, a6.y, a6.z, a6.w); En[7] = make_int4(a7.x, a7.y, a7.z, a7.w);
+                    }
                     asm volatile("" ::: "memory");
                 }
                 if constexpr (MODE == 3) {
@@ -151,7 +170,7 @@ __global__ void __launch_bounds__(256) bench(long long* out, int* sink, int nste
             asm volatile("s_mov_b64 %0, exec\n\ts_mov_b64 exec, %3\n\tds_write_b64 %1, %2\n\ts_mov_b64 exec, %0\n\ts_nop 4"
                          : "=&s"(saved) : "v"(oaddr), "v"(hx), "s"(0xffff000000000000ull) : "memory");
         }
-        if constexpr (EREAD || MODE == 2 || MODE == 3) {
+        if constexpr (EREAD || MODE == 2 || MODE == 3 || MODE == 12) {
 #pragma unroll
             for (int k = 0; k < 8; k++) E[k] = En[k];
         } else {
@@ -178,19 +197,19 @@ __global__ void __launch_bounds__(256) bench(long long* out, int* sink, int nste
 }
 
 template <typename F>
-double run(F kern, int blocks, int n) {
+double run(F kern, int blocks, int n, int threads = 256) {
     long long* d;
     int* s;
     (void)hipMalloc(&d, 16 * blocks * sizeof(long long));
-    (void)hipMalloc(&s, blocks * 256 * sizeof(int));
-    kern<<<blocks, 256>>>(d, s, n, 5, -1000);
-    kern<<<blocks, 256>>>(d, s, n, 5, -1000);
+    (void)hipMalloc(&s, blocks * threads * sizeof(int));
+    kern<<<blocks, threads>>>(d, s, n, 5, -1000);
+    kern<<<blocks, threads>>>(d, s, n, 5, -1000);
     (void)hipDeviceSynchronize();
     std::vector<long long> h(16 * blocks);
     (void)hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
     std::vector<double> v;
     for (int b = 0; b < blocks; b++)
-        for (int w = 0; w < 4; w++) v.push_back((double)h[b * 16 + w]);
+        for (int w = 0; w < threads / 64; w++) v.push_back((double)h[b * 16 + w]);
     std::sort(v.begin(), v.end());
     (void)hipFree(d);
     (void)hipFree(s);
@@ -208,6 +227,9 @@ void row() {
                            "+ DPP shift regs + b64 store", "+ 1 check / sub-chunk", "+ 1 check / block",
                            "r3: edges+prof+store+check", "r3 with seq window + v_perm"};
     for (size_t v = 0; v < fns.size(); v++) printf("TD=%d %-30s %6.1f cyc/step/wave\n", TD, modes[v], run(fns[v], 256, n));
+    printf("TD=%d %-30s %6.1f cyc/step/wave\n", TD, "+ exec-masked edge reads (wait)", run(bench<TD, 12>, 256, n));
+    printf("TD=%d %-30s %6.1f cyc/step/wave (2 waves/SIMD)\n", TD, "bare steps", run(bench<TD, 0>, 256, n, 512));
+    printf("TD=%d %-30s %6.1f cyc/step/wave (2 waves/SIMD)\n", TD, "r3: edges+prof+store+check", run(bench<TD, 10>, 256, n, 512));
 }
 
 int main() {
