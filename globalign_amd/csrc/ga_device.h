@@ -52,9 +52,10 @@ struct FillArgs {
     // tuning overrides from the context's knobs (ga_ctx::knobs; < 0: the default): LDS floor per workgroup
     // (GA_FILL_LDS_FLOOR), lane-fill sub-chunk steps score only (GA_LANE_SUB) / with words (GA_LANE_TB_SUB)
     int lds_floor, lane_sub, lane_tb_sub;
-    int asm_step;             // lane fill, score only: 1 the lean asm sub-chunk, 2 the round-3 asm steps, 0 the compiler's
-                              // (ga_lane_asm.h; GA_LANE_ASM)
+    int asm_step;             // lane fill, score only: the lean asm sub-chunk (ga_lane_asm.h LaneSub), else the compiler's
+                              // steps (GA_LANE_ASM=0)
     int io_prio;              // lane fill: s_setprio of the IO and profile waves (GA_LANE_IOPRIO; 0: none)
+    int hand_scope;           // lane fill: workgroup hand-off polls with system-scope loads (1), and stores (2)
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),

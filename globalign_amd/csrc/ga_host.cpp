@@ -821,6 +821,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.asm_step = e ? atoi(e) : 1;
         e = c->knob("GA_LANE_IOPRIO");
         p.io_prio = e ? atoi(e) : 0;
+        e = c->knob("GA_LANE_HANDSCOPE");
+        p.hand_scope = e ? atoi(e) : 0;
     }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);

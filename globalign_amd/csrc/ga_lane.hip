@@ -106,21 +106,33 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         int2* rin0 = ring;
         const int2* rout = ring + nlive * RING;
         const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
-        unsigned in_next = 0, out_next = 0, spins = 0, in_win = 64;
+        unsigned in_next = 0, out_next = 0, spins = 0, in_win = 192;
         while (in_next < (unsigned)m || out_next < (unsigned)m) {
             bool moved = false;
             if (in_next < (unsigned)m && in_sent) {
                 const unsigned cap = min(min(lds_ld(&cnt[0]) + RING, (unsigned)m), in_next + in_win);
                 if (cap > in_next) {
                     // one sc1 round trip per poll; while the writer is behind, its next 16 rows (the writer's
-                    // last compute wave stores a 16-step sub-chunk's rows at a time), else up to 64
+                    // last compute wave stores a 16-step sub-chunk's rows at a time), else up to 192 (three loads
+                    // per lane in flight together): the chain writes a row every ~40 ns and a round trip under load
+                    // takes 1-3 us, so a 64-row poll fell behind on some links and their lag grew over the whole
+                    // fill (lane stamps: end lags up to 128 us at workgroup boundaries)
                     const unsigned r = in_next + 1 + lane;
-                    const int2 e1 = r <= cap ? unpack64(g_ld64(src + r)) : make_int2(HAND_SENT, 0);
-                    const unsigned long long ok = __ballot(e1.x != HAND_SENT);
-                    const unsigned k = ~ok ? (unsigned)__builtin_ctzll(~ok) : 64u;
-                    in_win = k >= cap - in_next ? 64u : 16u;
+                    // (GA_LANE_HANDSCOPE >= 1: system-scope loads, past every cache, for the experiments)
+                    auto hld = [&](const int2* a) { return unpack64(p.hand_scope ? s_ld64(a) : g_ld64(a)); };
+                    const int2 e1 = r <= cap ? hld(src + r) : make_int2(HAND_SENT, 0);
+                    const int2 e2 = r + 64 <= cap ? hld(src + r + 64) : make_int2(HAND_SENT, 0);
+                    const int2 e3 = r + 128 <= cap ? hld(src + r + 128) : make_int2(HAND_SENT, 0);
+                    const unsigned long long ok1 = __ballot(e1.x != HAND_SENT), ok2 = __ballot(e2.x != HAND_SENT),
+                                             ok3 = __ballot(e3.x != HAND_SENT);
+                    unsigned k = ~ok1 ? (unsigned)__builtin_ctzll(~ok1) : 64u;
+                    if (k == 64u) k += ~ok2 ? (unsigned)__builtin_ctzll(~ok2) : 64u;
+                    if (k == 128u) k += ~ok3 ? (unsigned)__builtin_ctzll(~ok3) : 64u;
+                    in_win = k >= cap - in_next ? 192u : 16u;
                     if (k > 0) {
                         if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
+                        if (lane + 64 < (int)k) rin0[(r + 63) & RMASK] = e2;
+                        if (lane + 128 < (int)k) rin0[(r + 127) & RMASK] = e3;
                         const unsigned hi = in_next + k;
                         if (lane == 0) lds_st(&cnt[LK_PROD0], hi == (unsigned)m ? LK_DONE : hi);
                         in_next = hi;
@@ -156,14 +168,18 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                 }
             } else if (out_next < (unsigned)m) {
                 const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
-                const unsigned hi = min(min(P, (unsigned)m), out_next + 64);
+                // up to 192 rows a pass (a pass waits for the in-path's poll round trip too)
+                const unsigned hi = min(min(P, (unsigned)m), out_next + 192);
                 if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
-                    const unsigned r = out_next + 1 + lane;
-                    if (r <= hi) {
-                        const int2 e = rout[(r - 1) & RMASK];
-                        if (out_sent) g_st64(dst + r, e);
-                        else s_st64(dst + r, e);  // another GPU's halo
-                        if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
+#pragma unroll
+                    for (int h = 0; h < 3; h++) {
+                        const unsigned r = out_next + 1 + lane + 64 * h;
+                        if (r <= hi) {
+                            const int2 e = rout[(r - 1) & RMASK];
+                            if (out_sent && p.hand_scope < 2) g_st64(dst + r, e);
+                            else s_st64(dst + r, e);  // another GPU's halo
+                            if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
+                        }
                     }
                     if (!out_sent) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -288,12 +304,6 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     // lean sub-chunk, and register allocation then runs for tens of minutes)
     constexpr bool ASMOK = CB == 0 && !CKP && SUB == 16 && (NWC == 4 || TD <= 2);
     const bool use_asm = ASMOK && p.asm_step;
-    // asm sub-chunks keep lane 63's rows in registers (no DPP shift registers): the RC right-edge checkpoints
-    // and the direct hand-off read them back from the output ring (lanes 0..15) and store them one sub-chunk
-    // later, when the read has long landed
-    int2 pend_v = make_int2(0, 0);
-    int pend_row = 0;
-    bool pend_hand = false;  // the pending rows (GA_LANE_ASM=2 sub-chunks) also go to the hand-off rows
     unsigned* prod_in = w == 0 ? &cnt[LK_PROD0] : &cnt[2 * w - 1];
     // the workgroup's last compute wave writes the hand-off rows (not a slab's halo to another GPU, which
     // the IO wave streams with its progress word)
@@ -301,19 +311,6 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     const bool hand_direct = p.hand_direct && w == nlive - 1 && !(last_slab_w && p.edge_out != nullptr);
     int2* hand_out = p.hand + (long long)g * (m + 1);
     const bool last_full = last_slab_w && p.n % (64 * TD) == 0;
-    auto flush_pend = [&]() {
-        if (ASMOK && pend_row > 0) {
-            const int row = pend_row + lane;
-            if (lane < SUB && row >= 1 && row <= m) {
-                if (RC && p.colck != nullptr) p.colck[(long long)s * (m + 1) + row] = pend_v;
-                if (hand_direct && pend_hand) {
-                    g_st64(hand_out + row, pend_v);
-                    if (row == m && last_full) p.out_last[0] = pend_v.x;  // H'(m, n): the cost
-                }
-            }
-            pend_row = 0;
-        }
-    };
     unsigned* cons_out = &cnt[2 * w + 2];
     unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
@@ -450,7 +447,6 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
             };
             one(std::integral_constant<int, 0>{});
             qloads();
-            flush_pend();
             if constexpr (LE > 0) {
                 LkUnroll<1, LE>::run(one);
                 eloads();
@@ -477,7 +473,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         } else {
             const bool masked = r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB;
             if constexpr (ASMOK) {
-                if (use_asm && !masked && p.asm_step == 1) {
+                if (use_asm && !masked) {
                     // The lean sub-chunk: the 16 steps, the next sub-chunk's profile and edge reads
                     // and lane 63's rows out as ONE asm statement (LaneSub, ga_lane_asm.h), so that no compiler code,
                     // copy or conservative wait sits between the steps.  Lane 63's rows go out by DPP moves into
@@ -514,7 +510,10 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                         const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin + ((r0 + SUB) & RMASK)) : ezero;
 #pragma unroll
                         for (int k = 0; k < NE; k++) Nx[k] = src[k];
-                        asm volatile("" ::: "memory");
+                        // landed inside this branch, so that the compiler's wait is not at the merge (where it would
+                        // also wait for the lean statement's row stores on every sub-chunk)
+#pragma unroll
+                        for (int k = 0; k < NE; k++) asm volatile("" ::"v"(Nx[k].x), "v"(Nx[k].y), "v"(Nx[k].z), "v"(Nx[k].w));
                     } else {
 #pragma unroll
                         for (int k = 0; k < NE; k++) Nx[k] = make_int4(En[k].x, En[k].y, En[k].z, En[k].w);
@@ -537,58 +536,6 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                                 if (row == m && last_full) p.out_last[0] = v.x;  // H'(m, n): the cost
                             }
                         }
-                    }
-                    return;
-                }
-                if (use_asm && !masked) {
-                    // (GA_LANE_ASM=2) the round-3 asm sub-chunk: lane 63's rows of this sub-chunk stay in registers
-                    // (the asm step's hn / ex)
-                    int oh[SUB], ox[SUB];
-                    // steps 4d+u0 .. 4d+u0+n-1 (profile dwords d) in one asm statement
-                    auto blk = [&](auto D, auto U0, auto N) {
-                        constexpr int d = decltype(D)::value, u0 = decltype(U0)::value, n = decltype(N)::value;
-                        constexpr int u = 4 * d + u0;
-                        uint32_t qq[TD];
-#pragma unroll
-                        for (int k = 0; k < TD; k++) qq[k] = qc[k][d];
-                        LaneAsm<TD, u0, n>::run(H, Y, Xl, HLp, eh + u, ex + u, qq, o, oh + u, ox + u);
-                    };
-                    using I0 = std::integral_constant<int, 0>;
-                    using I1 = std::integral_constant<int, 1>;
-                    using I2 = std::integral_constant<int, 2>;
-                    using I3 = std::integral_constant<int, 3>;
-                    using I4 = std::integral_constant<int, 4>;
-                    static_assert(LE == 0 || LE == 13, "asm sub-chunk layout");
-                    if constexpr (LE == 13) {
-                        blk(I0{}, I0{}, I4{});
-                        qloads();
-                        flush_pend();
-                        blk(I1{}, I0{}, I4{});
-                        blk(I2{}, I0{}, I4{});
-                        blk(I3{}, I0{}, I1{});
-                        eloads();
-                        blk(I3{}, I1{}, I3{});
-                    } else {
-                        blk(I0{}, I0{}, I1{});
-                        qloads();
-                        eloads();
-                        flush_pend();
-                        blk(I0{}, I1{}, I3{});
-                        blk(I1{}, I0{}, I4{});
-                        blk(I2{}, I0{}, I4{});
-                        blk(I3{}, I0{}, I4{});
-                    }
-                    Hl = H[TD - 1];
-                    const int rlo = r0 - 62;
-                    if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
-                    const unsigned b1 = rout_lds + (unsigned)((rlo - 1) & RMASK) * 8u;
-                    const unsigned b2 = rout_lds + (unsigned)((rlo - 1 + SUB - 1) & RMASK) * 8u;
-                    const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
-                    lk_store_rows(b1, b2, pc_lds, cp, oh, ox);
-                    if ((RC && p.colck != nullptr) || hand_direct) {
-                        pend_row = rlo;
-                        pend_hand = true;
-                        pend_v = rout[(rlo - 1 + (lane & (SUB - 1))) & RMASK];
                     }
                     return;
                 }
@@ -684,7 +631,6 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
             }
         }
     }
-    flush_pend();  // the last asm sub-chunk's read-back rows
     unsigned* prod_out = &cnt[2 * w + 1];
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
     if (partial && lane == cn / TD) p.out_last[0] = Hm;

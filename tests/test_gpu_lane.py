@@ -182,14 +182,12 @@ def test_lane_traceback_banded(monkeypatch, td, band_rows):
     _align_lane(monkeypatch, s1, s2, SCORING, seed=7 + band_rows, td=td, band_rows=band_rows)
 
 
-@pytest.mark.parametrize("env", [{}, {"GA_LANE_ASM": "2"}, {"GA_LANE_DIRECT": "1"},
-                                 {"GA_LANE_DIRECT": "1", "GA_LANE_ASM": "2"}, {"GA_LANE_ASM": "0"},
+@pytest.mark.parametrize("env", [{}, {"GA_LANE_DIRECT": "1"}, {"GA_LANE_DIRECT": "1", "GA_LANE_ASM": "0"}, {"GA_LANE_ASM": "0"},
                                  {"GA_LANE_LATE": "0"}])
 @pytest.mark.parametrize("td", [1, 2, 4])
 def test_lane_handover_variants(monkeypatch, env, td):
     """The edge hand-over variants over a chain of many workgroups with a partial last stripe:
-    the lean asm sub-chunk (default) and the
-    round-3 asm steps (GA_LANE_ASM=2), the IO wave's workgroup hand-off and the last compute wave's direct one
+    the lean asm sub-chunk (default), the IO wave's workgroup hand-off and the last compute wave's direct one
     (GA_LANE_DIRECT=1), the compiler's step (GA_LANE_ASM=0), early edge reads (GA_LANE_LATE=0)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)

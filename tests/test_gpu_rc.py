@@ -60,11 +60,10 @@ def test_rc_stripe_widths_vs_oracle(monkeypatch, td):
     assert kind[1] == td
 
 
-@pytest.mark.parametrize("env", [{"GA_LANE_ASM": 2}, {"GA_LANE_DIRECT": 1}, {"GA_LANE_DIRECT": 1, "GA_LANE_ASM": 2},
-                                 {"GA_LANE_ASM": 0}])
+@pytest.mark.parametrize("env", [{"GA_LANE_DIRECT": 1}, {"GA_LANE_DIRECT": 1, "GA_LANE_ASM": 0}, {"GA_LANE_ASM": 0}])
 def test_rc_handover_variants_vs_oracle(monkeypatch, env):
     """The checkpointing fill under each edge hand-over: the right-edge checkpoints are read back
-    from lanes 48..63 of the lean sub-chunk or read back from the output ring (GA_LANE_ASM=2)."""
+    from lanes 48..63 of the lean sub-chunk or from the compiler steps' DPP shift registers (GA_LANE_ASM=0)."""
     _align(monkeypatch, splitmix_seq(3100, 51, "dna"), splitmix_seq(64 * 2 * 4 * 5 + 77, 52, "dna"), DNA, seed=3,
            env=dict(env, GA_LANE_COLS_PER_LANE=2))
 

@@ -64,6 +64,10 @@ for sd in range(4):
                                                                  (m + 63)))}
 by_wave = {int(w): {"wait_edge_frac": float(np.median(st[wave_in_wg == w, 2] / tot[wave_in_wg == w])),
                     "simd_mode": int(np.bincount(simd[wave_in_wg == w]).argmax())} for w in range(min(nwc, ns))}
+if os.environ.get("LANE_STAMPS_DUMP"):
+    # the raw per-stripe stamps: start, end (s_memrealtime), wait cycles (edges, profile, ring space), total cycles,
+    # HW_ID, XCC_ID
+    np.save(os.environ["LANE_STAMPS_DUMP"], st)
 xcc = st[:, 7] & 0xF
 xcross = xcc[1:] != xcc[:-1]
 pct = {f"p{q}": float(np.percentile(elag, q)) for q in (10, 50, 90, 99)} if len(elag) else {}
