@@ -80,14 +80,35 @@ def hottest_loop(body, skip_op=None):
     return best
 
 
+def asm_block_ops(body, op):
+    """VALU ops of the largest inline-asm statement (;;#ASMSTART .. ;;#ASMEND) holding `op`: the lane kernel's lean
+    sub-chunk (ga_lane_asm.h LaneSub), which is its whole steady-state step stream"""
+    best, cur, inside = [], [], False
+    for l in body:
+        t = l.strip()
+        if t.startswith(";;#ASMSTART"):
+            inside, cur = True, []
+        elif t.startswith(";;#ASMEND"):
+            inside = False
+            if any(x.startswith(op) for x in cur) and len(cur) > len(best):
+                best = cur
+        elif inside and t.startswith("v_"):
+            cur.append(t.split()[0])
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
     ap.add_argument("symbol")
     ap.add_argument("--json")
     ap.add_argument("--skip-blocks-with", default=None, help="drop basic blocks of the loop holding this op")
+    ap.add_argument("--asm-block-with", default=None, help="price the largest inline-asm statement holding this op")
     a = ap.parse_args()
-    lo, hi, ops = hottest_loop(kernel_body(a.asm, a.symbol), a.skip_blocks_with)
+    if a.asm_block_with:
+        lo, hi, ops = -1, -1, asm_block_ops(kernel_body(a.asm, a.symbol), a.asm_block_with)
+    else:
+        lo, hi, ops = hottest_loop(kernel_body(a.asm, a.symbol), a.skip_blocks_with)
     hist = collections.Counter(ops)
     cyc = sum(cost(o)[0] * c for o, c in hist.items())
     unmeasured = sorted({o for o in hist if not cost(o)[1]})
@@ -95,7 +116,8 @@ def main():
     out = {"symbol": a.symbol, "loop_lines": [lo, hi], "valu_ops_in_loop": len(ops),
            "simd_cycles_in_loop": cyc, "mean_simd_cycles_per_op": mean,
            "peak_valu_insts_per_s": 256 * 4 * 2.4e9 / mean, "unmeasured_forms_priced_at_v_min_i32": unmeasured,
-           "skipped_blocks_with": a.skip_blocks_with, "histogram": dict(hist.most_common())}
+           "skipped_blocks_with": a.skip_blocks_with, "asm_block_with": a.asm_block_with,
+           "histogram": dict(hist.most_common())}
     print(json.dumps(out, indent=1))
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
