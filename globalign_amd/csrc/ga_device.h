@@ -43,7 +43,8 @@ struct FillArgs {
     int2* ckpt;               // banded traceback: (H', h2') of rows ckpt_rows, 2*ckpt_rows, ... (< m) or nullptr
     int ckpt_rows;            //   [row / ckpt_rows - 1][n + 1]; a multiple of FROWS
     // recompute checkpoints of the lane fill (nullptr: none)
-    int2* colck;              // [nstripes][m + 1]: (H', h1') of every stripe's right edge column, rows 1..m
+    int2* colck;              // [nstripes][m + 1]: (H', h1') of every stripe's right edge column, rows 1..m; then 64
+                              // scratch slots (the lean sub-chunk's lanes that carry no row store there)
     int2* stck;               // staircase lane states after step k*stck_every - 1, k = 1 .. (m - 1) / stck_every:
                               //   [k - 1][nstripes][TD + 1][64]: (H'[c], h2'[c]) for c < TD, then (h1' carry, H' diag)
     int stck_every;           //   a multiple of 32 (a pair of 16-step sub-chunks)
@@ -55,6 +56,7 @@ struct FillArgs {
     int asm_step;             // lane fill, score only: the lean asm sub-chunk (ga_lane_asm.h LaneSub), else the compiler's
                               // steps (GA_LANE_ASM=0)
     int io_prio;              // lane fill: s_setprio of the IO and profile waves (GA_LANE_IOPRIO; 0: none)
+    int out_wave;             // lane fill (NWC <= 4): the out-path in a wave of its own (GA_LANE_OUTWAVE; 0: the IO wave's)
     int hand_scope;           // lane fill: workgroup hand-off polls with system-scope loads (1), and stores (2)
 };
 

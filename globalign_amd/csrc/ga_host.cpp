@@ -27,6 +27,7 @@
 
 #include "../../include/globalign_amd.h"
 #include "ga_device.h"
+#include "ga_lane.h"
 
 namespace {
 
@@ -823,10 +824,12 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.io_prio = e ? atoi(e) : 0;
         e = c->knob("GA_LANE_HANDSCOPE");
         p.hand_scope = e ? atoi(e) : 0;
+        e = c->knob("GA_LANE_OUTWAVE");
+        p.out_wave = e ? atoi(e) : 1;
     }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);
-        for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * (size_t)c->nstripes * (m + 1)},
+        for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * ((size_t)c->nstripes * (m + 1) + 64)},
                                   {&c->stck, sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64}})
             if (const hipError_t e = buf->ensure(bytes); e != hipSuccess) {
                 (void)hipGetLastError();
@@ -869,7 +872,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (const char* e = c->knob("GA_HALO_SPIN_LIMIT")) p.halo_spin_limit = (unsigned)std::max(1L, atol(e));  // (tests)
     // a slab with a left neighbour: every wait of its fill is, in the end, a wait for that halo
     if (c->slab && c->col0 > 0) p.spin_limit = std::max(p.spin_limit, p.halo_spin_limit);
-    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * 8 * c->nstripes));
+    if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * ga::LK_DBG_WORDS * c->nstripes));
+    if (c->dbg_on) HIPCHK(hipMemsetAsync(c->dbg.p, 0, sizeof(unsigned long long) * ga::LK_DBG_WORDS * c->nstripes, st));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
     if (c->lane) ga::launch_fill_lane(st, p, c->CB);
@@ -2612,7 +2616,7 @@ int ga_debug_stamps(ga_ctx* c, int enable, unsigned long long* out, int64_t cap)
     if (!c) return fail(GA_E_ARG, "null context");
     c->dbg_on = enable != 0;
     if (out && c->dbg.p) {
-        const int64_t nb = std::min<int64_t>(cap, 8 * (int64_t)c->nstripes);
+        const int64_t nb = std::min<int64_t>(cap, ga::LK_DBG_WORDS * (int64_t)c->nstripes);
         HIPCHK(hipMemcpy(out, c->dbg.p, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost));
     }
     return GA_OK;

@@ -21,7 +21,16 @@ constexpr int LK_SCR_OFF = LK_ZERO_OFF + 16 * 8;
 constexpr int LK_HEAD_BYTES = LK_SCR_OFF + 64 * 8;
 constexpr int LK_QMIRROR = 16;  // profile slots mirrored past the ring's end (a window reads idx .. idx+12)
 constexpr unsigned LK_DONE = 0x7fffffffu;
+// DBG stamps per stripe (tools/lane_stamps.py): start, end, wait cycles (edges, profile, ring space), total cycles,
+// HW_ID, XCC_ID; the row-m/2 probe: edge row known landed, own row published, (the workgroup's first stripe) landed
+// in ring 0 by the IO wave, (its last stripe) stored to HBM by the out-path
+constexpr int LK_DBG_WORDS = 12;
 typedef unsigned lk_v2u __attribute__((ext_vector_type(2)));
+// waves of a lane-fill workgroup: NWC compute waves, the IO wave, the profile wave and, for NWC <= 4, an out wave that
+// only moves the last compute wave's rows to HBM (at NWC = 8 a third extra wave would put three waves on a SIMD and
+// cap every wave at 168 VGPRs)
+constexpr bool lane_out_wave(int nwc) { return nwc <= 4; }
+constexpr int lane_block_threads(int nwc) { return 64 * (nwc + (lane_out_wave(nwc) ? 3 : 2)); }
 
 
 // traceback code of a cell (CB bytes, W = (8*CB-1)/2 bits per field; fill_kernel's TbFmt): the

@@ -59,7 +59,8 @@ size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
 // more cycles per step): for one-round chains (C3, slabs), whose time is m steps plus every stripe's lag;
 // fills in rounds (C4 on one GPU) run uncoupled and keep the early reads
 template <int NWC, int TD, int CB, int SUB, bool DBG, bool CKP = false, bool RC = false, bool LATE = false>
-__global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
+__global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(FillArgs p) {
+    constexpr bool OUTW = lane_out_wave(NWC);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     unsigned* cnt = reinterpret_cast<unsigned*>(smem);
     int2* ring = reinterpret_cast<int2*>(smem + LK_HEAD_BYTES);
@@ -94,19 +95,85 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         else if (p.io_prio == 2) __builtin_amdgcn_s_setprio(2);
         else if (p.io_prio == 1) __builtin_amdgcn_s_setprio(1);
     };
+    // the out-path (the last compute wave's ring -> HBM) runs in a wave of its own when the workgroup has one
+    // (OUTW, p.out_wave): in the IO wave a pass waited behind every in-path poll's round trip
+    const bool own_out = OUTW && p.out_wave;
+    const bool last_slab = g == p.nslabs - 1;
+    const bool out_sent = !(last_slab && p.edge_out != nullptr);
+    // one out-path pass: up to 192 rows from the last compute wave's ring to HBM; true if it moved any
+    auto out_pass = [&](unsigned& out_next) -> bool {
+        int2* dst = out_sent ? p.hand + (long long)g * (m + 1) : p.edge_out;
+        const int2* rout = ring + nlive * RING;
+        if (out_sent && p.hand_direct) {
+            // the last compute wave stores its right edge to the hand-off rows itself (sub_chunk): only
+            // its ring slots are freed here
+            const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
+            if (P > out_next) {
+                lds_st(&cnt[2 * nlive], P);
+                out_next = min(P, (unsigned)m);
+                return true;
+            }
+            return false;
+        }
+        const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
+        // up to 192 rows a pass
+        const unsigned hi = min(min(P, (unsigned)m), out_next + 192);
+        if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
+#pragma unroll
+            for (int h = 0; h < 3; h++) {
+                const unsigned r = out_next + 1 + lane + 64 * h;
+                if (r <= hi) {
+                    const int2 e = rout[(r - 1) & RMASK];
+                    if (out_sent && p.hand_scope < 2) g_st64(dst + r, e);
+                    else s_st64(dst + r, e);  // another GPU's halo
+                    if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
+                }
+            }
+            if (!out_sent) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store(p.edge_prog, hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (lane == 0) lds_st(&cnt[2 * nlive], hi);
+            if (DBG && lane == 0 && out_next < (unsigned)(m / 2) && hi >= (unsigned)(m / 2))
+                p.dbg[LK_DBG_WORDS * (g * NWC + nlive - 1) + 11] = __builtin_amdgcn_s_memrealtime();
+            out_next = hi;
+            return true;
+        }
+        return false;
+    };
+    if (OUTW && w == NWC + 2) {
+        // ---------------- out wave ----------------
+        if (!own_out) return;
+        io_prio();
+        unsigned out_next = 0, spins = 0;
+        while (out_next < (unsigned)m) {
+            if (out_pass(out_next)) {
+                spins = 0;
+            } else {
+                if (__hip_atomic_load(abort_sh, RLX, WGS)) {
+                    g_st(p.abort_word, 1u);
+                    break;
+                }
+                if (!spin_ok(spins, p.spin_limit, p.abort_word)) {
+                    __hip_atomic_store(abort_sh, 1u, RLX, WGS);
+                    break;
+                }
+            }
+        }
+        // gave up before the right edge was complete: tell the reader of the edge (the next slab's fill)
+        if (!out_sent && out_next < (unsigned)m && p.edge_prog != nullptr && lane == 0) s_prog_abort(p.edge_prog);
+        return;
+    }
     if (w == NWC) {
-        // ---------------- IO wave: edges HBM <-> LDS rings ----------------
+        // ---------------- IO wave: edges HBM -> LDS ring (and LDS ring -> HBM without an out wave) ----------------
         io_prio();
         const int2* src = g == 0 ? p.left : p.hand + (long long)(g - 1) * (m + 1);
         const unsigned* src_prog = g == 0 ? p.left_prog : nullptr;
         const unsigned limit = (g == 0 && p.left_prog != nullptr) ? p.halo_spin_limit : p.spin_limit;
         const bool src_sc1 = p.left_prog != nullptr;
-        const bool last_slab = g == p.nslabs - 1;
-        int2* dst = (last_slab && p.edge_out != nullptr) ? p.edge_out : p.hand + (long long)g * (m + 1);
         int2* rin0 = ring;
-        const int2* rout = ring + nlive * RING;
-        const bool in_sent = g > 0, out_sent = !(last_slab && p.edge_out != nullptr);
-        unsigned in_next = 0, out_next = 0, spins = 0, in_win = 192;
+        const bool in_sent = g > 0;
+        unsigned in_next = 0, out_next = own_out ? (unsigned)m : 0u, spins = 0, in_win = 192;
         while (in_next < (unsigned)m || out_next < (unsigned)m) {
             bool moved = false;
             if (in_next < (unsigned)m && in_sent) {
@@ -135,6 +202,8 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                         if (lane + 128 < (int)k) rin0[(r + 127) & RMASK] = e3;
                         const unsigned hi = in_next + k;
                         if (lane == 0) lds_st(&cnt[LK_PROD0], hi == (unsigned)m ? LK_DONE : hi);
+                        if (DBG && lane == 0 && in_next < (unsigned)(m / 2) && hi >= (unsigned)(m / 2))
+                            p.dbg[LK_DBG_WORDS * (g * NWC) + 10] = __builtin_amdgcn_s_memrealtime();
                         in_next = hi;
                         moved = true;
                     }
@@ -157,39 +226,8 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                     moved = true;
                 }
             }
-            if (out_next < (unsigned)m && out_sent && p.hand_direct) {
-                // the last compute wave stores its right edge to the hand-off rows itself (sub_chunk): only
-                // its ring slots are freed here
-                const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
-                if (P > out_next) {
-                    lds_st(&cnt[2 * nlive], P);
-                    out_next = min(P, (unsigned)m);
-                    moved = true;
-                }
-            } else if (out_next < (unsigned)m) {
-                const unsigned P = lds_ld(&cnt[2 * nlive - 1]);
-                // up to 192 rows a pass (a pass waits for the in-path's poll round trip too)
-                const unsigned hi = min(min(P, (unsigned)m), out_next + 192);
-                if (hi > out_next && (hi - out_next >= GOUT || hi == (unsigned)m)) {
-#pragma unroll
-                    for (int h = 0; h < 3; h++) {
-                        const unsigned r = out_next + 1 + lane + 64 * h;
-                        if (r <= hi) {
-                            const int2 e = rout[(r - 1) & RMASK];
-                            if (out_sent && p.hand_scope < 2) g_st64(dst + r, e);
-                            else s_st64(dst + r, e);  // another GPU's halo
-                            if (last_slab && r == (unsigned)m && p.n % (64 * TD) == 0) p.out_last[0] = e.x;
-                        }
-                    }
-                    if (!out_sent) {
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (lane == 0) __hip_atomic_store(p.edge_prog, hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                    if (lane == 0) lds_st(&cnt[2 * nlive], hi);
-                    out_next = hi;
-                    moved = true;
-                }
-            }
+            // (a pass here waits for the in-path's poll round trip too)
+            if (out_next < (unsigned)m && out_pass(out_next)) moved = true;
             if (!moved) {
                 if (__hip_atomic_load(abort_sh, RLX, WGS)) {
                     g_st(p.abort_word, 1u);
@@ -204,7 +242,8 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
             }
         }
         // gave up before the right edge was complete: tell the reader of the edge (the next slab's fill)
-        if (!out_sent && out_next < (unsigned)m && p.edge_prog != nullptr && lane == 0) s_prog_abort(p.edge_prog);
+        if (!own_out && !out_sent && out_next < (unsigned)m && p.edge_prog != nullptr && lane == 0)
+            s_prog_abort(p.edge_prog);
         return;
     }
     if (w == NWC + 1) {
@@ -314,9 +353,14 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     unsigned* cons_out = &cnt[2 * w + 2];
     unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
+    // the recompute checkpoints' right edge of this stripe, and a scratch slot per lane past all of them
+    int2* const colck_s = RC && p.colck != nullptr ? p.colck + (long long)s * (m + 1) : nullptr;
+    int2* const colck_x = RC && p.colck != nullptr ? p.colck + ((long long)p.nstripes * (m + 1) + lane) : nullptr;
     unsigned avail = 0, outfree = 0, qavail = 0;
     bool aborted = false;
     unsigned long long wcyc[3] = {0, 0, 0}, t_start = 0, c_start = 0;
+    // DBG probe (row m/2): when this wave knew its edge row m/2 had landed, when it published its own row m/2
+    unsigned long long t_avail = 0, t_pub = 0;
     if (DBG) {
         t_start = __builtin_amdgcn_s_memrealtime();
         c_start = __builtin_amdgcn_s_memtime();
@@ -473,7 +517,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
         } else {
             const bool masked = r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB;
             if constexpr (ASMOK) {
-                if (use_asm && !masked) {
+                if (use_asm && !masked && !hand_direct) {
                     // The lean sub-chunk: the 16 steps, the next sub-chunk's profile and edge reads
                     // and lane 63's rows out as ONE asm statement (LaneSub, ga_lane_asm.h), so that no compiler code,
                     // copy or conservative wait sits between the steps.  Lane 63's rows go out by DPP moves into
@@ -503,6 +547,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                     int R[4];
                     LaneSub<TD, LE ? 12 : 0>::run(H, Y, Xl, HLp, Ev, qc, o, ca_lds, ea, qbv, wa, wb, wc, cp, cv, En, qn, R);
                     Hl = H[TD - 1];
+                    if (DBG && rlo <= m / 2 && m / 2 < rlo + SUB) t_pub = __builtin_amdgcn_s_memrealtime();
                     const int need = min(r0 + 2 * SUB, m);
                     if ((int)sgpr_u(cv) < need) {
                         wait_ge(prod_in, 0, avail, need, 0);
@@ -518,6 +563,7 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
 #pragma unroll
                         for (int k = 0; k < NE; k++) Nx[k] = make_int4(En[k].x, En[k].y, En[k].z, En[k].w);
                     }
+                    if (DBG && r0 + SUB < m / 2 && m / 2 <= r0 + 2 * SUB) t_avail = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
                     for (int k = 0; k < TD; k++) {
                         qx[k][0] = qn[k][0].x;
@@ -525,17 +571,13 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
                         qx[k][2] = qn[k][1].x;
                         qx[k][3] = qn[k][1].y;
                     }
-                    if ((RC && p.colck != nullptr) || hand_direct) {
-                        // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge
+                    if (RC && p.colck != nullptr) {
+                        // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge; every lane stores (lanes
+                        // without a row into the scratch slots past the checkpoints): no exec change, which would
+                        // drain the VALU pipeline on every sub-chunk (the direct hand-off takes the compiler's steps)
                         const int row = rlo + lane - 48;
                         const int2 v = (lane & 4) ? make_int2(R[0], R[1]) : make_int2(R[2], R[3]);
-                        if (hi && row >= 1 && row <= m) {
-                            if (RC && p.colck != nullptr) p.colck[(long long)s * (m + 1) + row] = v;
-                            if (hand_direct) {
-                                g_st64(hand_out + row, v);
-                                if (row == m && last_full) p.out_last[0] = v.x;  // H'(m, n): the cost
-                            }
-                        }
+                        *(hi && row <= m ? colck_s + row : colck_x) = v;
                     }
                     return;
                 }
@@ -635,7 +677,9 @@ __global__ void __launch_bounds__(64 * (NWC + 2)) fill_lane_kernel(FillArgs p) {
     if (lane == 0) __hip_atomic_store(prod_out, LK_DONE, RLX, WGS);
     if (partial && lane == cn / TD) p.out_last[0] = Hm;
     if (DBG && lane == 0) {
-        unsigned long long* d = p.dbg + 8 * s;
+        unsigned long long* d = p.dbg + LK_DBG_WORDS * s;
+        d[8] = t_avail;
+        d[9] = t_pub;
         d[0] = t_start;
         d[1] = __builtin_amdgcn_s_memrealtime();
         d[2] = wcyc[0];
@@ -662,7 +706,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.stck != nullptr) {
             auto* fc = fill_lane_kernel<NWC, TD, 0, 16, false, false, true, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
+            fc<<<dim3(p.nslabs), dim3(lane_block_threads(NWC)), lds, s>>>(p);
             return;
         }
     }
@@ -670,7 +714,7 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.ckpt != nullptr) {  // 8-step sub-chunks: with 16 the checkpoint stores spill at TD >= 4
             auto* fc = fill_lane_kernel<NWC, TD, CB, 8, false, true>;
             (void)hipFuncSetAttribute((const void*)fc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fc<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
+            fc<<<dim3(p.nslabs), dim3(lane_block_threads(NWC)), lds, s>>>(p);
             return;
         }
     }
@@ -678,13 +722,13 @@ static void launch_lane_one(hipStream_t s, const FillArgs& p) {
         if (p.late) {
             auto* fl = fill_lane_kernel<NWC, TD, 0, 16, DBG, false, false, true>;
             (void)hipFuncSetAttribute((const void*)fl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            fl<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
+            fl<<<dim3(p.nslabs), dim3(lane_block_threads(NWC)), lds, s>>>(p);
             return;
         }
     }
     auto* fn = fill_lane_kernel<NWC, TD, CB, SUB, DBG>;
     (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    fn<<<dim3(p.nslabs), dim3(64 * (NWC + 2)), lds, s>>>(p);
+    fn<<<dim3(p.nslabs), dim3(lane_block_threads(NWC)), lds, s>>>(p);
 }
 
 // variants without spills (vgpr_spill_count of the code object; lane_geometry keeps to them): score

@@ -37,10 +37,11 @@ plain_ms = eng.kernel_ms()[0]
 L.ga_debug_stamps(eng._h, 1, None, 0)
 cost, _ = eng.fill(traceback=False)
 kind, T, ns, nwc, nslabs = eng.fill_kind()
-buf = np.zeros(8 * ns, dtype=np.uint64)
+W = 12  # LK_DBG_WORDS (ga_lane.h)
+buf = np.zeros(W * ns, dtype=np.uint64)
 L.ga_debug_stamps(eng._h, 0, buf.ctypes.data, buf.size)
 L.ga_debug_stamps(eng._h, 0, None, 0)
-st = buf.reshape(ns, 8).astype(np.int64)
+st = buf.reshape(ns, W).astype(np.int64)
 t0 = st[:, 0].min()
 start, end = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0  # microseconds (100 MHz)
 dur = end - start
@@ -78,7 +79,28 @@ dist = {"end_lag_pct_us": pct, "end_lag_max_us": float(elag.max()) if len(elag) 
         "cross_wg_links": {"same_xcd": int((cross & ~xcross).sum()), "other_xcd": int((cross & xcross).sum())},
         "end_lag_top": [{"stripe": int(i + 1), "lag_us": float(elag[i]), "wave": int((i + 1) % nwc),
                          "cross": bool(cross[i]), "xcd": [int(xcc[i]), int(xcc[i + 1])]} for i in top]}
+# the row-m/2 probe: per link s -> s+1, from the producer's publish of row m/2 to the consumer's
+# knowing it landed; cross-workgroup links through the out-path's store and the IO wave's landing in ring 0
+probe = {}
+if (st[:, 8] > 0).all() and (st[:, 9] > 0).all():
+    pub, avail = (st[:, 9] - t0) / 100.0, (st[:, 8] - t0) / 100.0
+    link = avail[1:] - pub[:-1]
+    probe["pub_to_avail_us"] = {"intra": float(np.median(link[~cross])) if (~cross).any() else None,
+                                "cross": float(np.median(link[cross])) if cross.any() else None}
+    ci = np.nonzero(cross)[0]
+    if len(ci) and (st[ci, 11] > 0).all() and (st[ci + 1, 10] > 0).all():
+        stored, landed = (st[ci, 11] - t0) / 100.0, (st[ci + 1, 10] - t0) / 100.0
+        probe["cross_parts_us"] = {"pub_to_stored": float(np.median(stored - pub[ci])),
+                                   "stored_to_landed": float(np.median(landed - stored)),
+                                   "landed_to_avail": float(np.median(avail[ci + 1] - landed))}
+        probe["cross_parts_mean_us"] = {"pub_to_stored": float(np.mean(stored - pub[ci])),
+                                        "stored_to_landed": float(np.mean(landed - stored)),
+                                        "landed_to_avail": float(np.mean(avail[ci + 1] - landed))}
+    # the consumer's own publish of row m/2 after it knew its edge row landed (the stripe's skew + batching)
+    own = pub - avail
+    probe["avail_to_own_pub_us"] = float(np.median(own))
 print(json.dumps({
+    "probe_m2": probe,
     "m": m, "n": n, "cost": int(cost), "kind": kind, "TD": T, "nstripes": ns, "nwc": nwc, "nslabs": nslabs,
     "fill_ms_plain": plain_ms, "fill_ms_dbg": eng.kernel_ms()[0],
     "last_end_us": float(end.max()), "last_start_us": float(start.max()),

@@ -17,10 +17,10 @@ import json
 O = "gpurun_out/r4_end"
 for f in ("bench_default", "bench_c5", "bench_c2", "bench_c4tb"):
     d = json.loads(open(f"{O}/{f}.json").read().strip().splitlines()[-1])
-    r = d.get("roofline", {})
+    r = d.get("roofline") or {}
     s = f"{f}: value {d['value']:.4g} ms/step {d['ms_per_step']:.3f} fill {d.get('fill_ms', 0):.3f} walk {d.get('walk_ms', 0):.3f} kind {d.get('fill_kind')} frac {r.get('frac')} achieved {r.get('achieved')}"
     if "c4" in d:
         s += f" | C4 {d['c4']['fill_ms']:.2f} ok {d['c4']['cost_matches_oracle']} frac {d['c4']['roofline'].get('frac')}"
-    pin = d["config"].get("traceback_pin", {}).get("matches_oracle")
+    pin = (d["config"].get("traceback_pin") or {}).get("matches_oracle")
     print(s, "pin", pin, "cost_ok", d["config"].get("cost_matches_oracle"))
 PY
