@@ -56,6 +56,7 @@ struct FillArgs {
     int asm_step;             // lane fill, score only: the lean asm sub-chunk (ga_lane_asm.h LaneSub), else the compiler's
                               // steps (GA_LANE_ASM=0)
     int io_prio;              // lane fill: s_setprio of the IO and profile waves (GA_LANE_IOPRIO; 0: none)
+    int poll_win;             // lane fill: rows per hand-off poll (GA_LANE_POLLWIN, <= 192; 0: 16 while the writer is behind, else 192)
     int out_wave;             // lane fill (NWC <= 4): the out-path in a wave of its own (GA_LANE_OUTWAVE; 0: the IO wave's)
     int hand_scope;           // lane fill: workgroup hand-off polls with system-scope loads (1), and stores (2)
 };

@@ -688,6 +688,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // at TD 4: 284 + 90 ms, tools/exp/r3b_c4tb3.sh, r3b_c4rc.py)
         if (c->T > 4 && !c->lane_T_req && !lane_geometry(c, n, &qrows, false, 4, 4))
             return fail(GA_E_STATE, "recompute fill geometry");
+        // and 4 where the geometry model chose fewer (round 4, the lean sub-chunk): fewer, wider stripes shorten
+        // the ramp as much as their slower step lengthens the rows, and the walk's blocks come cheaper (C3: fill
+        // 9.69 -> 9.81 ms, walk 5.72 -> 5.42; C5 3.92 against 6.3 ms at TD = 1; tools/r4_td.sh)
+        // Not with a narrow recompute window (GA_RC_WIN < 16, tests): its few likeliest candidates at TD = 4 all lie
+        // in the walker's own stripe, and one worker behind a 4-block window starved the walk of the stripe to the
+        // left (test_rc_worker_pools_vs_oracle[env0] timed out)
+        const char* rw = c->knob("GA_RC_WIN");
+        if (c->T < 4 && !c->lane_T_req && (!rw || atoi(rw) >= 16)) (void)lane_geometry(c, n, &qrows, false, 4, 4);
         // The checkpoint spacing, with the stripes' geometry known: the smallest (<= 4096 steps) whose states
         // fit the memory budget (default 96 GB of the 288: C4 on one GPU, TD 4, takes 128 steps, 78 GB; 64
         // would take 156 GB and walks no faster) and whose worker fits LDS; GA_RC_EVERY fixes it (the stripes
@@ -824,6 +832,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.io_prio = e ? atoi(e) : 0;
         e = c->knob("GA_LANE_HANDSCOPE");
         p.hand_scope = e ? atoi(e) : 0;
+        e = c->knob("GA_LANE_POLLWIN");
+        p.poll_win = e ? std::min(std::max(atoi(e), 0), 192) : 0;
         e = c->knob("GA_LANE_OUTWAVE");
         p.out_wave = e ? atoi(e) : 1;
     }
@@ -1224,9 +1234,10 @@ bool rc_eligible(ga_ctx* c) {
     if (mode == 0 || c->slab || c->qbytes != 1 || c->K > 32) return false;
     if (c->m < 256 || c->n < 256) return false;  // (degenerate walks read cells no block ever recomputes)
     if (mode == 1) return true;
-    // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
-    // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
-    int64_t min_cells = (int64_t)1 << 32;
+    // 2^26 cells and up (round 4): with the lean sub-chunk and 4-column stripes the recompute call beats the
+    // stored-words one from C2 up (one call: C2 2.00 -> 1.75-1.77 ms, C5 4.12 -> 3.92, C3 15.73 -> 15.57;
+    // tools/r4_td.sh, profiles/r04/single_call_td.txt); in round 3 C5's recompute fill at TD = 1 took 4.8 ms
+    int64_t min_cells = (int64_t)1 << 26;
     if (const char* t = c->knob("GA_RC_MIN_CELLS")) min_cells = atoll(t);
     return c->m * c->n >= min_cells;
 }

@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                     unsigned k = ~ok1 ? (unsigned)__builtin_ctzll(~ok1) : 64u;
                     if (k == 64u) k += ~ok2 ? (unsigned)__builtin_ctzll(~ok2) : 64u;
                     if (k == 128u) k += ~ok3 ? (unsigned)__builtin_ctzll(~ok3) : 64u;
-                    in_win = k >= cap - in_next ? 192u : 16u;
+                    in_win = p.poll_win > 0 ? (unsigned)p.poll_win : k >= cap - in_next ? 192u : 16u;
                     if (k > 0) {
                         if (lane < (int)k) rin0[(r - 1) & RMASK] = e1;
                         if (lane + 64 < (int)k) rin0[(r + 63) & RMASK] = e2;
