@@ -526,6 +526,8 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                     // executes a wave's operations in order, the producer writes rows before its counter) and only a
                     // producer that really is behind costs a poll and a re-read.
                     const int rlo = r0 - 62;
+                    // (a wave-uniform test: compared in a VGPR, the compiler masked exec around the wait, twice a sub-chunk)
+                    outfree = sgpr_u(outfree);
                     if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
                     lk_v4i Ev[NE];
 #pragma unroll
@@ -577,7 +579,11 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                         // drain the VALU pipeline on every sub-chunk (the direct hand-off takes the compiler's steps)
                         const int row = rlo + lane - 48;
                         const int2 v = (lane & 4) ? make_int2(R[0], R[1]) : make_int2(R[2], R[3]);
-                        *(hi && row <= m ? colck_s + row : colck_x) = v;
+                        // one 8-byte store in asm: the compiler split `*p = v` into two dword stores and put the second
+                        // under an exec mask
+                        int2* const cdst = hi && row <= m ? colck_s + row : colck_x;
+                        const lk_v2u vv = {(unsigned)v.x, (unsigned)v.y};
+                        asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(cdst), "v"(vv) : "memory");
                     }
                     return;
                 }
