@@ -407,12 +407,23 @@ def knob_fingerprint():
     return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("GA_")))
 
 
+def evict_stale(cache, key):
+    """Drop the cached entries of key's (device(s), thread) whose GA_* fingerprint differs from key's: a context
+    made under other knobs is never asked for again by this thread, and its device buffers (traceback words,
+    checkpoints, tile cache) would otherwise stay allocated and shrink the free memory later calls size
+    themselves by.  The context is destroyed once nothing else holds it (Engine.__del__)."""
+    for k in [k for k in cache if k[:2] == key[:2] and k != key]:
+        del cache[k]
+
+
 def default_engine(device=0):
-    """Process-wide engine per device and GA_* override set (contexts are not thread-safe: one per thread)."""
+    """Process-wide engine per device and GA_* override set (contexts are not thread-safe: one per thread);
+    one set per (device, thread) is kept, the current one."""
     key = (device, threading.get_ident(), knob_fingerprint())
     with _default_lock:
         eng = _default.get(key)
         if eng is None:
+            evict_stale(_default, key)
             eng = Engine(device)
             _default[key] = eng
         return eng

@@ -59,6 +59,7 @@ struct FillArgs {
     int poll_win;             // lane fill: rows per hand-off poll (GA_LANE_POLLWIN, <= 192; 0: 16 while the writer is behind, else 192)
     int out_wave;             // lane fill (NWC <= 4): the out-path in a wave of its own (GA_LANE_OUTWAVE; 0: the IO wave's)
     int hand_scope;           // lane fill: workgroup hand-off polls with system-scope loads (1), and stores (2)
+    int xcd_map;              // lane fill, one round of workgroups: chain neighbours on one XCD (ga_lane.hip lane_slab)
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),

@@ -318,6 +318,16 @@ struct ga_ctx {
         const auto it = knobs.find(name);
         return it == knobs.end() ? nullptr : it->second.c_str();
     }
+    // knobs of paths that were measured and dropped: read only by an experiments build
+    // (make EXPERIMENTS=1); the shipped library ignores them
+    const char* xknob(const char* name) const {
+#ifdef GA_EXPERIMENTS
+        return knob(name);
+#else
+        (void)name;
+        return nullptr;
+#endif
+    }
     int device = 0;
     int priority = 0;  // of `stream` (the greatest the device offers, see ga_ctx_create)
     hipStream_t stream = nullptr;
@@ -627,6 +637,16 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     return GA_OK;
 }
 
+// Device memory a buffer may take: hipMemGetInfo's free bytes plus `held` (what the context's own buffers being
+// resized already hold), less a 2 GB margin; GA_DEV_AVAIL_MB caps it (tests: forces the fallbacks).
+int64_t dev_avail_bytes(ga_ctx* c, int64_t held) {
+    int64_t avail = INT64_MAX / 4;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) avail = (int64_t)fr + held - ((int64_t)2 << 30);
+    if (const char* e = c->knob("GA_DEV_AVAIL_MB")) avail = std::min<int64_t>(avail, atoll(e) << 20);
+    return std::max<int64_t>(avail, 0);
+}
+
 // A band of rows of the whole problem (banded traceback): rows r0+1 .. r0+mb, its
 // top row from a checkpoint (nullptr: row 0), no boundary pass; or the checkpointing pass itself.
 struct Band {
@@ -691,11 +711,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // and 4 where the geometry model chose fewer (round 4, the lean sub-chunk): fewer, wider stripes shorten
         // the ramp as much as their slower step lengthens the rows, and the walk's blocks come cheaper (C3: fill
         // 9.69 -> 9.81 ms, walk 5.72 -> 5.42; C5 3.92 against 6.3 ms at TD = 1; tools/r4_td.sh)
-        // Not with a narrow recompute window (GA_RC_WIN < 16, tests): its few likeliest candidates at TD = 4 all lie
-        // in the walker's own stripe, and one worker behind a 4-block window starved the walk of the stripe to the
-        // left (test_rc_worker_pools_vs_oracle[env0] timed out)
-        const char* rw = c->knob("GA_RC_WIN");
-        if (c->T < 4 && !c->lane_T_req && (!rw || atoi(rw) >= 16)) (void)lane_geometry(c, n, &qrows, false, 4, 4);
+        if (c->T < 4 && !c->lane_T_req) (void)lane_geometry(c, n, &qrows, false, 4, 4);
         // The checkpoint spacing, with the stripes' geometry known: the smallest (<= 4096 steps) whose states
         // fit the memory budget (default 96 GB of the 288: C4 on one GPU, TD 4, takes 128 steps, 78 GB; 64
         // would take 156 GB and walks no faster) and whose worker fits LDS; GA_RC_EVERY fixes it (the stripes
@@ -706,13 +722,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // GA_E_NOMEM, and ga_problem_align takes the banded traceback instead.
         int64_t budget = (int64_t)96 << 30;
         if (const char* e = c->knob("GA_RC_BUDGET_MB")) budget = atoll(e) << 20;
-        int64_t dev_avail = INT64_MAX;
-        {
-            size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess)
-                dev_avail = (int64_t)fr + (int64_t)c->stck.cap + (int64_t)c->colck.cap + (int64_t)c->rc_tb.cap -
-                            ((int64_t)2 << 30);
-        }
+        const int64_t dev_avail = dev_avail_bytes(c, (int64_t)c->stck.cap + (int64_t)c->colck.cap + (int64_t)c->rc_tb.cap);
         auto ck_bytes = [&](int e) {
             const int64_t nck = std::max<int64_t>((m - 1) / e, 1);
             return nck * c->nstripes * (c->T + 1) * 512;
@@ -816,6 +826,12 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     // one round of lane workgroups (every stripe resident): the chain's lag counts, read edges late
     p.late = c->lane && c->nslabs <= c->num_cu ? 1 : 0;
     if (const char* e = c->knob("GA_LANE_LATE")) p.late = atoi(e);
+    // chain neighbours on one XCD (ga_lane.hip lane_slab; experiments build only): measured no faster, since ticket
+    // order already keeps 165 of C3's 195 cross-workgroup links on one XCD (r5: 188 with the map; C3 fill 9.43 ->
+    // 9.46 ms, tools/exp/r5/xcd.sh).  Only for one round of workgroups that runs alone (a pipeline's fills share
+    // the device; a fill that finds its workgroups not all resident falls back to ticket order after ~40 us)
+    p.xcd_map = 0;
+    if (const char* e = c->xknob("GA_LANE_XCD")) p.xcd_map = c->lane && c->nslabs <= c->num_cu && bd.stream == nullptr ? atoi(e) : 0;
     p.hand_direct = 0;  // measured: C4 210 ms against 221 with the direct hand-off, 1M x 125k 52.5 against 56 (r3_c4.log)
     if (const char* e = c->knob("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
     p.stck_every = every;
@@ -828,9 +844,9 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         p.lane_tb_sub = e ? atoi(e) : -1;
         e = c->knob("GA_LANE_ASM");
         p.asm_step = e ? atoi(e) : 1;
-        e = c->knob("GA_LANE_IOPRIO");
+        e = c->xknob("GA_LANE_IOPRIO");
         p.io_prio = e ? atoi(e) : 0;
-        e = c->knob("GA_LANE_HANDSCOPE");
+        e = c->xknob("GA_LANE_HANDSCOPE");
         p.hand_scope = e ? atoi(e) : 0;
         e = c->knob("GA_LANE_POLLWIN");
         p.poll_win = e ? std::min(std::max(atoi(e), 0), 192) : 0;
@@ -839,13 +855,27 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     }
     if (bd.rc) {
         const int64_t nck = std::max<int64_t>((m - 1) / every, 1);
+        // An allocation that fails (the size check above passed, but the device's free memory moved) releases every
+        // recompute buffer before GA_E_NOMEM, so the fallback (ga_problem_align: banded / stored words) sizes
+        // itself with that memory free.  The boundary pass and the memsets enqueued above are harmless: the
+        // fallback's own fill enqueues them again behind them on the same stream.  GA_RC_FAIL_ALLOC=1 (tests)
+        // fails the second allocation after the first succeeded.
+        const bool fail_test = c->knob("GA_RC_FAIL_ALLOC") && atoi(c->knob("GA_RC_FAIL_ALLOC")) == 1;
+        int nb = 0;
         for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * ((size_t)c->nstripes * (m + 1) + 64)},
-                                  {&c->stck, sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64}})
-            if (const hipError_t e = buf->ensure(bytes); e != hipSuccess) {
+                                  {&c->stck, sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64}}) {
+            hipError_t e = buf->ensure(bytes);
+            if (e == hipSuccess && fail_test && nb == 1) e = hipErrorOutOfMemory;
+            nb++;
+            if (e != hipSuccess) {
                 (void)hipGetLastError();
+                c->colck.release();
+                c->stck.release();
+                c->rc_tb.release();
                 return fail(e == hipErrorOutOfMemory ? GA_E_NOMEM : GA_E_HIP,
                             std::string("recompute checkpoints: ") + hipGetErrorString(e));
             }
+        }
         p.colck = c->colck.as<int2>();
         p.stck = c->stck.as<int2>();
     }
@@ -991,12 +1021,12 @@ ga::WalkArgs walk_args(ga_ctx* c, int64_t ntab, const WalkStart& st, int64_t r0,
         // the loaders leave the 4x4 tile block's far off-diagonal corners: 28 % fewer
         // speculative tile loads, C3 walk 6.87 -> 6.71 ms alone and 7.74 -> 7.4 ms in the pipeline, C5
         // 1.45 -> 1.27 ms (tools/exp/walk_skip.sh); GA_WALK_SKIP_CORNERS = 0 / 2 / 3 for none / more
-        const char* e = c->knob("GA_WALK_SKIP_CORNERS");
+        const char* e = c->xknob("GA_WALK_SKIP_CORNERS");
         w.skip_corners = e ? atoi(e) : 1;
         // 14 loader waves (the L2 prefetcher's and the idle wave's too): tile waits at C3 469 -> 186 us
         // alone, 921 -> 413 us in the pipeline, walk 6.81 -> 6.52 ms alone, C5 1.28 -> 1.15 ms
         // (tools/exp/walk_loaders.sh); GA_WALK_LOADERS = 12 / 13 for the former roles
-        const char* nl = c->knob("GA_WALK_LOADERS");
+        const char* nl = c->xknob("GA_WALK_LOADERS");
         w.nloaders = nl ? atoi(nl) : 14;
     }
     w.ops = wb.ops;
@@ -1155,6 +1185,9 @@ int64_t band_rows(ga_ctx* c) {
     }
     int64_t budget = (int64_t)64 << 30;
     if (const char* e = c->knob("GA_TB_BUDGET_MB")) budget = atoll(e) << 20;
+    // ... and no more than the device has free for them (what this context's word buffer already holds counts as
+    // free), less a 2 GB margin: a stored-words fill past it failed with GA_E_HIP instead of banding
+    budget = std::min(budget, dev_avail_bytes(c, (int64_t)c->tb.cap));
     const int64_t words = ((c->n + 63) / 64) * 64 * c->CB;  // traceback bytes per row
     if (c->m * words <= budget) return 0;
     const int64_t Bh = std::max<int64_t>(64, (budget / words / ga::FROWS) * ga::FROWS);
@@ -1284,7 +1317,7 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     // 14 loaders, no L2 prefetcher (it would read blocks not yet recomputed); GA_RC_LOADERS = 12 / 13 leave
     // waves 8 and 12 / wave 8 (the walker's SIMD) idle instead
     w.nloaders = 14;
-    if (const char* e = c->knob("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
+    if (const char* e = c->xknob("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
     w.rc_flags = c->rc_flags.as<unsigned>();
     w.rc_ready = 2u * c->rc_epoch + 1u;
     w.rc_nbs = nbs;
@@ -1335,6 +1368,12 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         std::vector<std::pair<int, int>> off;
         for (int di = 0; di < span; di++)
             for (int dj = 0; dj < span; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
+        // Liveness whatever the window's width: the walker waits only on tiles of its block and of the blocks
+        // above it, left of it and up-left (its verified 2 x 2 tiles), so those four rank first (key -1);
+        // ranked by the key alone, a 4-block window at TD = 4 held the walker's own stripe only, and one worker
+        // never recomputed the stripe to its left (test_rc_worker_pools_vs_oracle[env0] timed out, round 4)
+        for (auto& o : off)
+            if (o.first == 0 || o.first == 1 || o.first == 16 || o.first == 17) o.second = -1;
         std::stable_sort(off.begin(), off.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
             return x.second < y.second;
         });
@@ -1537,7 +1576,7 @@ int pipe_setup(ga_ctx* c) {
         // masked out of the fill streams it never waits for one to drain, and two fills may share the
         // other CUs (GA_PIPE_WALK_CUS, default 0: unmasked streams)
         int wc = 0;
-        if (const char* e = c->knob("GA_PIPE_WALK_CUS")) wc = std::max(0, std::min(8, atoi(e)));
+        if (const char* e = c->xknob("GA_PIPE_WALK_CUS")) wc = std::max(0, std::min(8, atoi(e)));
         c->walk_cus = wc;
         if (wc > 0) {
             const int nc = c->num_cu, words = (nc + 31) / 32;
@@ -1924,7 +1963,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
         const char* ch = c->knob("GA_PIPE_CHAIN");
         const bool fits = (int64_t)count * (c->m + c->n + 1) <= ((int64_t)256 << 20);  // 1 GB of entries
         const bool on = ch != nullptr && atoi(ch) != 0;
-        if (on && fits && c->walk_cus == 0 && !c->knob("GA_PIPE_FILL_PRIO") && !c->knob("GA_PIPE_ROW_FIRST"))
+        if (on && fits && c->walk_cus == 0 && !c->knob("GA_PIPE_FILL_PRIO") && !c->xknob("GA_PIPE_ROW_FIRST"))
             return align_chain(c, count, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out, t0);
     }
     const int64_t m = c->m, n = c->n, per = m + n + 1;
@@ -1959,7 +1998,7 @@ int align_many(ga_ctx* c, int count, uint32_t* mt_state, const char* a_chr, cons
     double walk_launch_host = 0.0;
     // experiment (GA_PIPE_ROW_FIRST=r): the first r fills through the row scan (shorter latency alone)
     int row_first = 0;
-    if (const char* e = c->knob("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
+    if (const char* e = c->xknob("GA_PIPE_ROW_FIRST")) row_first = atoi(e);
     // fill j into slot j % S on fill stream j % F; each computes its own boundary.  Every fill of the
     // pipeline computes the same arrays (the same pair, boundary and words), so walk k takes whichever
     // pending slot's fill ended first, not slot k % S: in the ramp the third of four fills started at
@@ -2323,7 +2362,8 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     c->rc_used = false;
     if (rc_eligible(c)) {
         const int r = rc_align(c, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
-        // checkpoints that do not fit this device (nothing was enqueued): the banded traceback below
+        // checkpoints that do not fit this device (refused before anything was enqueued, or an allocation that
+        // failed, after which the recompute buffers are released): the banded / stored-words paths below
         if (r != GA_E_NOMEM) return r;
         c->rc_used = false;
     }

@@ -38,6 +38,45 @@
 
 namespace ga {
 
+// The slab (chain position) of this workgroup; thread 0 only.  Ticket order by default: a later slab never
+// waits on one whose workgroup is not yet running.  p.xcd_map (one round of workgroups, every stripe resident):
+// the hardware dispatches workgroup h to XCD h mod 8, so consecutive tickets sit on different XCDs and every
+// cross-workgroup hand-off crossed the non-coherent L2 boundary (540 against 385 ns one way,
+// profiles/r04/micro_handoff_lat.txt).  Instead the slabs are cut into one contiguous run per XCD, in XCD
+// order, each run as long as the number of workgroups that XCD received: 7 links cross XCDs instead of
+// nslabs - 1.  That order is safe only with every workgroup resident, so it is used only once all have
+// arrived (the last to arrive says so); if they have not within ~40 us (the device busy with other work),
+// the first to give up switches every workgroup to ticket order (one CAS decides).
+// Flags: [0] arrivals (the ticket), [2] mode (0 pending, 1 per XCD, 2 tickets), [4 + x] arrivals on XCD x.
+__device__ unsigned lane_slab(const FillArgs& p) {
+    unsigned* F = p.ticket;
+    if (!p.xcd_map) return atomicAdd(F, 1u);
+    const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;  // HW_REG_XCC_ID bits 3:0
+    const unsigned rk = __hip_atomic_fetch_add(F + 4 + x, 1u, __ATOMIC_RELAXED, AGENT);
+    // the per-XCD count first: once the last arrival is seen every count is final
+    const unsigned arr = __hip_atomic_fetch_add(F, 1u, __ATOMIC_ACQ_REL, AGENT);
+    unsigned mode = 0;
+    if (arr == (unsigned)p.nslabs - 1u) {
+        unsigned exp = 0;
+        mode = __hip_atomic_compare_exchange_strong(F + 2, &exp, 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE, AGENT) ? 1u : exp;
+    } else {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while ((mode = __hip_atomic_load(F + 2, __ATOMIC_ACQUIRE, AGENT)) == 0u) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 4000) {  // 40 us (100 MHz)
+                unsigned exp = 0;
+                mode = __hip_atomic_compare_exchange_strong(F + 2, &exp, 2u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE, AGENT)
+                           ? 2u : exp;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    if (mode != 1u) return arr;
+    unsigned start = 0;
+    for (unsigned y = 0; y < x; y++) start += __hip_atomic_load(F + 4 + y, __ATOMIC_RELAXED, AGENT);
+    return start + rk;
+}
+
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
     return (size_t)LK_HEAD_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + LK_QMIRROR) * 4 +
            (size_t)K * 32;  // + the K x K int8 sub' table (K <= 32)
@@ -77,7 +116,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     if (threadIdx.x < 32) reinterpret_cast<unsigned*>(smem + LK_ZERO_OFF)[threadIdx.x] = 0u;  // the zero block
     for (int q = threadIdx.x; q < K * K; q += blockDim.x) stab[(q / K) * 32 + q % K] = (int8_t)p.subp[q];
     __syncthreads();
-    if (threadIdx.x == 0) cnt[LK_SLAB] = atomicAdd(p.ticket, 1u);
+    if (threadIdx.x == 0) cnt[LK_SLAB] = lane_slab(p);
     __syncthreads();
     const int g = __builtin_amdgcn_readfirstlane((int)cnt[LK_SLAB]);
     const int m = p.m, o = p.o;

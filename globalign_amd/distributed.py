@@ -360,6 +360,7 @@ def device_engines(devices):
     with _device_engines_lock:
         engines = _device_engines.get(key)
         if engines is None:
+            _native.evict_stale(_device_engines, key)
             engines = [GpuSlabEngine(d) for d in devices]
             _device_engines[key] = engines
         return engines

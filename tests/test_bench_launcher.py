@@ -22,8 +22,10 @@ def _run(args, **env):
                           text=True, timeout=600)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_spawns_ranks_gloo(n):
+    """World sizes up to the driver's 8-GPU node: 8 ranks over gloo (C1's 1000 columns cut into slabs as narrow as
+    one column: the orchestration's edge cases)."""
     r = _run(["--gpus", str(n), "--workload", "c1", "--steps", "2", "--warmup", "1"], GA_DIST_BACKEND="gloo",
              GA_BENCH_ENGINE="tests.bench_cpu_engine:make_engine")
     assert r.returncode == 0, r.stderr[-3000:]

@@ -76,8 +76,11 @@ def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback
 
 
 @pytest.mark.parametrize("edge", ["ipc", "bands"])
-@pytest.mark.parametrize("world,m,n,seed,band", [(2, 3000, 5000, 21, 512), (3, 2100, 4100, 8, 700)])
+@pytest.mark.parametrize("world,m,n,seed,band", [(2, 3000, 5000, 21, 512), (3, 2100, 4100, 8, 700),
+                                                  (8, 1500, 8 * 512, 31, 512)])
 def test_gpu_slabs_edge_modes_match_oracle(world, m, n, seed, band, edge, tmp_path, monkeypatch):
+    """World sizes 2, 3 and 8 (the driver's 8-GPU node: here 8 rank processes share the MI355X, one 512-column
+    slab each, seven links, the walk handed over seven times)."""
     monkeypatch.setenv("GA_SLAB_EDGE", edge)
     _slabs_match_oracle(world, m, n, seed, band, tmp_path)
 

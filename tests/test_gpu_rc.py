@@ -78,8 +78,11 @@ def test_rc_checkpoint_spacing_vs_oracle(monkeypatch, every):
                                  {"GA_RC_SERVERS": 2, "GA_RC_WIN": 64, "GA_RC_WPW": 6},
                                  {"GA_RC_SERVERS": 160, "GA_RC_WPW": 4}])
 def test_rc_worker_pools_vs_oracle(monkeypatch, env):
-    """One worker behind a narrow window, a few many-worker groups, many groups racing for claims."""
-    _align(monkeypatch, splitmix_seq(2500, 41, "dna"), splitmix_seq(2600, 42, "dna"), DNA, seed=7, env=env)
+    """One worker behind a narrow window, a few many-worker groups, many groups racing for claims.  Every pool at
+    the default 4 columns per lane: the window always offers the walker's own 2 x 2 blocks first, so even one
+    worker behind a 4-block window never starves it of the stripe to its left (round 4 kept this case at TD < 4)."""
+    kind = _align(monkeypatch, splitmix_seq(2500, 41, "dna"), splitmix_seq(2600, 42, "dna"), DNA, seed=7, env=env)
+    assert kind[1] == 4, kind
 
 
 @pytest.mark.parametrize("o", [7, 130])
@@ -190,3 +193,44 @@ def test_rc_checkpoints_over_budget_fall_back(monkeypatch):
     assert kind[0] != "rc", kind
     assert status == 0 and int(cost) == ref["cost"] and tuple(strings) == tuple(ref["strings"])
     assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+
+
+def _align_fallback(monkeypatch, env, seed):
+    """A problem the recompute walk would take, under `env` that makes it decline: the call must fall back and
+    still equal the oracle (cost, strings, random state)."""
+    from globalign_amd import _native
+    from globalign_amd.scoring import validate_and_transform_args
+    from oracle import core, transform
+    s1, s2 = splitmix_seq(1500, 61 + seed, "dna"), splitmix_seq(1700, 62 + seed, "dna")
+    a1, a2, smat, cmat, gos, goc = transform.settings(dict(DNA, seq_1=s1, seq_2=s2))
+    random.seed(seed)
+    mt = np.array(random.getstate()[1], dtype=np.uint32)
+    ref = core.align(a1, a2, cmat, goc, mt)
+    _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **DNA)
+    tables = _native.CostTables(cmat2, goc2)
+    monkeypatch.setenv("GA_RC", "1")
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    eng = _native.Engine(0)
+    try:
+        eng.load(tables.codes(a1), tables.codes(a2), tables)
+        for _ in range(2):  # the fallback twice on one context: nothing of the declined path is left behind
+            cost, strings, status, mt_after = eng.align(mt, a1, a2)
+            assert eng.fill_kind()[0] != "rc"
+            assert status == 0 and int(cost) == ref["cost"]
+            assert tuple(strings) == tuple(ref["strings"])
+            assert np.asarray(mt_after, dtype=np.uint32).tolist() == np.asarray(ref["mt_out"], dtype=np.uint32).tolist()
+    finally:
+        eng.close()
+
+
+def test_rc_checkpoint_alloc_failure_falls_back(monkeypatch):
+    """a checkpoint allocation that fails after the other succeeded (GA_RC_FAIL_ALLOC=1) releases the
+    recompute buffers and falls back to the stored-words path."""
+    _align_fallback(monkeypatch, {"GA_RC_FAIL_ALLOC": 1}, seed=1)
+
+
+def test_small_device_memory_bands(monkeypatch):
+    """With little free device memory (GA_DEV_AVAIL_MB caps what the sizing sees) the recompute walk declines and
+    the traceback words are banded to fit, instead of a stored-words fill that cannot allocate."""
+    _align_fallback(monkeypatch, {"GA_DEV_AVAIL_MB": 1}, seed=2)

@@ -85,3 +85,43 @@ def test_tiebreak_stream_resumes_exactly(lib, seed, steps, chunk):
     s3 = np.zeros(625, np.uint32)
     assert lib.ga_debug_rng(s2.ctypes.data, steps - G, fresh.ctypes.data, 0, s3.ctypes.data, C.byref(ms)) == 0
     assert fresh.tolist() == one[G:].tolist()
+
+
+def test_lane_asm_header_matches_generator(tmp_path):
+    """The committed ga_lane_asm.h is exactly what tools/gen_lane_asm.py generates (no hand edits, no drift)."""
+    import subprocess
+    import sys
+    out = tmp_path / "ga_lane_asm.h"
+    subprocess.check_call([sys.executable, f"{ROOT}/tools/gen_lane_asm.py", str(out)], stdout=subprocess.DEVNULL)
+    assert out.read_bytes() == open(f"{ROOT}/globalign_amd/csrc/ga_lane_asm.h", "rb").read()
+
+
+def test_engine_cache_keeps_one_knob_set(monkeypatch):
+    """default_engine / device_engines keep one context per (device(s), thread): a GA_* change drops the contexts
+    made under the old set (they held their device buffers for the life of the process)."""
+    import gc
+    import weakref
+
+    from globalign_amd import _native, distributed
+
+    made = []
+
+    class FakeEngine:
+        def __init__(self, device):
+            self.device = device
+            made.append(weakref.ref(self))
+
+    monkeypatch.setattr(_native, "Engine", FakeEngine)
+    monkeypatch.setattr(_native, "_default", {})
+    monkeypatch.setattr(distributed, "_device_engines", {})
+    for k in range(5):
+        monkeypatch.setenv("GA_RC_SERVERS", str(48 + k))
+        e0 = _native.default_engine(0)
+        assert _native.default_engine(0) is e0          # same knobs: the cached context
+        _native.default_engine(1)
+        distributed.device_engines([0, 1])
+    assert len(_native._default) == 2                    # one per device for this thread
+    assert len(distributed._device_engines) == 1
+    del e0
+    gc.collect()
+    assert sum(r() is not None for r in made) == 4       # the current set's: 2 default + 2 slab engines

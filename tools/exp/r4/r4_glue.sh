@@ -5,7 +5,7 @@ O=gpurun_out/r4_glue
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_lane.py tests/test_gpu_rc.py -m gpu > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
-bash tools/r4_probe.sh || exit 1
+bash tools/exp/r4/r4_probe.sh || exit 1
 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c3.json 2> $O/c3.err || { tail -5 $O/c3.err; exit 1; }
 python3 -c "
 import json

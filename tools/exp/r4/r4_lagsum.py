@@ -1,6 +1,6 @@
-"""Summarise tools/r4_*.sh runs: lane-stamp lags (C3 shape, 1M x 125k slab) and the C3 bench line per variant.
+"""Summarise tools/exp/r4/r4_*.sh runs: lane-stamp lags (C3 shape, 1M x 125k slab) and the C3 bench line per variant.
 
-    python tools/r4_lagsum.py <dir> <variant> [<variant> ...]
+    python tools/exp/r4/r4_lagsum.py <dir> <variant> [<variant> ...]
 """
 import json
 import sys

@@ -10,4 +10,4 @@ for v in 1 0; do
   GA_LANE_OUTWAVE=$v GA_FILL_MODE=lane timeout -k 10 120 python -u tools/lane_stamps.py 1000000 125000 > $O/stamps_slab_$v.json 2> $O/stamps_slab_$v.err || { tail -5 $O/stamps_slab_$v.err; exit 1; }
   GA_LANE_OUTWAVE=$v timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 1; }
 done
-python3 tools/r4_lagsum.py $O 1 0
+python3 tools/exp/r4/r4_lagsum.py $O 1 0

@@ -2,7 +2,8 @@
 gfx950 asm, one specialisation per (TD columns per lane, profile byte U, leading nop), and the
 sub-chunk's row store from lane 63.
 
-    python tools/gen_lane_asm.py        (rewrites the header; the build uses the committed copy)
+    python tools/gen_lane_asm.py [out]  (rewrites the header, or writes `out`; the build uses the committed copy,
+                                         tests/test_host_cpu.py checks that it still matches this generator)
 
 A step of TD columns (the same int32 recurrence as ga_lane.h lane_step, Ho form):
     M_k  = Hd_k + sub'(a_i, b_j)      Hd_0 = HLp (the left lane's H' of the step before), Hd_k = H_{k-1}
@@ -212,7 +213,7 @@ __device__ __forceinline__ void lk_store_rows(unsigned b1, unsigned b2, unsigned
 """
 
 
-def main():
+def main(out=OUT):
     parts = ["""// ga_lane_asm.h -- GENERATED by tools/gen_lane_asm.py (do not edit): the lane-skewed fill's unmasked
 // score-only step as hand-scheduled gfx950 asm (DESIGN.md 5.6) and the sub-chunk's row store.
 #pragma once
@@ -238,10 +239,11 @@ struct LaneSub;
             parts.append(sub_chunk(td, rs))
     parts.append(store_rows())
     parts.append("}  // namespace ga\n")
-    with open(OUT, "w") as f:
+    with open(out, "w") as f:
         f.write("\n".join(parts))
-    print(OUT)
+    print(out)
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(sys.argv[1] if len(sys.argv) > 1 else OUT)
