@@ -316,6 +316,8 @@ def measure_single(wl, steps, warmup, pipelined=True):
             out["latency_ms"] = elapsed * 1e3 / steps
         out["mode"] = "one call per step"
     out["fill_kind"] = eng.fill_kind()
+    if wl["traceback"]:
+        out["walk_kind"] = eng.walk_kind()
     eng.close()
     cells = wl["m"] * wl["n"]
     out.update(elapsed=elapsed, cost=int(cost), cells=cells, value=cells * steps / elapsed,
@@ -370,6 +372,7 @@ def single_line(args, workload, wl):
         line["latency_ms_per_alignment"] = r["latency_ms"]
         line["step_mode"] = r["mode"]
         line["fill_kind"] = r.get("fill_kind")
+        line["walk_kind"] = r.get("walk_kind")  # 'jump': the tie-to-tie walk
         line["config"]["traceback_pin"] = traceback_pin(workload, r)
         if not args.no_extra:
             # the repeated-pair throughput mode (ga_problem_align_many: walk k beside fill k+1, stored words)

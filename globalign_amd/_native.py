@@ -238,6 +238,16 @@ class Engine:
         _check(f(self._h, out.ctypes.data))
         return (("row", "diag", "lane", "rc")[int(out[0])],) + tuple(int(x) for x in out[1:])
 
+    def walk_kind(self):
+        """The walk of the last traceback: 'stored' (traceback words), 'rc' (the recompute walk of words) or 'jump'
+        (the tie-to-tie recompute walk)."""
+        f = self._L.ga_debug_walk_kind
+        f.argtypes = [C.c_void_p, C.c_void_p]
+        f.restype = C.c_int
+        out = np.zeros(1, dtype=np.int32)
+        _check(f(self._h, out.ctypes.data))
+        return ("stored", "rc", "jump")[int(out[0])]
+
     def set_cells(self, cells):
         """Use a filled (m+1, n+1, 3) int32 cell array for the next traceback (-> min of the last cell)."""
         arr = np.ascontiguousarray(cells, dtype=np.int32)

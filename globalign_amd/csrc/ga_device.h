@@ -154,6 +154,11 @@ void launch_walk_chain(hipStream_t s, const WalkChainArgs& a);
 // the recompute walk: one walker workgroup + nserv recompute workgroups (ga_rcwalk.hip)
 void launch_walk_rc(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv);
 int rc_worker_bytes(int TD, int CB, int stck_every);
+// the tie-to-tie walk (ga_jump.h): the same launch with jump entries instead of traceback words
+// (TD <= 4, o <= 14); r.tb is then the entry cache (RC_CACHE_I x RC_CACHE_S blocks of 4*TD 6 KB tiles)
+void launch_walk_rc_jump(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv);
+int rc_jump_worker_bytes_host(int TD, int stck_every);
+size_t rc_jump_lds_bytes(int TD, int stck_every);  // LDS of a workgroup with one jump worker
 // traceback words of a caller-supplied (m+1) x (n+1) x 3 cell array (dp_array_backward shim)
 void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)

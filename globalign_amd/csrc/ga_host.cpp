@@ -419,6 +419,7 @@ struct ga_ctx {
     int64_t rc_ops_cap = 0;  // words
     unsigned* rc_ops_prog = nullptr;
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
+    bool rc_jump = false;  // the last recompute walk was the tie-to-tie walk (jump entries)
     int rc_every_used = 64;
 };
 
@@ -1296,12 +1297,24 @@ int rc_fill(ga_ctx* c) {
 
 // Launch the walk + recompute workgroups from walk state `st` on the walk buffers `wb` (its table already
 // uploaded), after rc_fill.
+constexpr bool kRcJumpDefault = false;  // the tie-to-tie walk unless GA_RC_JUMP says otherwise
+
 int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     const int64_t m = c->m, n = c->n;
     const int TD = c->rc_T, CB = c->CB;
     const int nbi = (int)((m + 63) / 64), nbs = c->nstripes;
+    // The tie-to-tie walk when its workers fit: at most 4 columns per lane (a worker stages its
+    // block's 3 x 64 x 64*TD entries in LDS) and o <= 14 (X'-H', Y'-H' saturated at o+1 index a 1024-entry LUT).
+    // GA_RC_JUMP=0 keeps the walk of traceback words.
+    {
+        const char* e = c->knob("GA_RC_JUMP");
+        c->rc_jump = (e ? atoi(e) != 0 : kRcJumpDefault) && TD <= 4 && c->o <= 14 &&
+                     ga::rc_jump_lds_bytes(TD, c->rc_every_used) + 12 * 1024 <= 160 * 1024;
+    }
+    if (c->rc_jump)
+        HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * 4 * TD * 6144 + 65536));
     // (+ one 64-column stripe of slack: a loader reads whole 1 KiB runs)
-    HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4));
+    else HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4));
     const size_t nflags = (size_t)nbi * nbs;
     if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_epoch >= 0x7ffffff0u) {
         HIPCHK(c->rc_flags.ensure(nflags * sizeof(unsigned)));
@@ -1347,10 +1360,10 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     r.epoch = c->rc_epoch;
     r.pos = c->rc_pos.as<unsigned>();
     r.tile0 = (int)((((st.i - 1) / 64) << 16) | ((st.j - c->col0 - 1) / 64));  // the walk's first tile
-    r.worker_bytes = ga::rc_worker_bytes(TD, CB, r.stck_every);
+    r.worker_bytes = c->rc_jump ? ga::rc_jump_worker_bytes_host(TD, r.stck_every) : ga::rc_worker_bytes(TD, CB, r.stck_every);
     // one worker per workgroup (one per CU) by default: C3 blocks 14.7 us against 16.5 at three per CU,
     // the walker's tile waits 0.07 against 0.5 ms (tools/exp/r3_rc_diag.py)
-    r.workers = std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
+    r.workers = c->rc_jump ? 1 : std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
     if (const char* e = c->knob("GA_RC_WPW")) r.workers = std::max(1, std::min(r.workers, atoi(e)));
     else r.workers = 1;
     r.spin_limit = 1u << 20;
@@ -1389,7 +1402,8 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     int nserv = 64;
     if (const char* e = c->knob("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
     HIPCHK(hipEventRecord(wb.ev0, wb.stream));
-    ga::launch_walk_rc(wb.stream, w, r, nserv);
+    if (c->rc_jump) ga::launch_walk_rc_jump(wb.stream, w, r, nserv);
+    else ga::launch_walk_rc(wb.stream, w, r, nserv);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(wb.ev1, wb.stream));
     return GA_OK;
@@ -2730,6 +2744,14 @@ int ga_debug_rc(ga_ctx* c, unsigned* out4) {
     if (!c || !out4) return fail(GA_E_ARG, "null argument");
     if (!c->rc_pos.p) return fail(GA_E_STATE, "no recompute walk ran");
     HIPCHK(hipMemcpy(out4, c->rc_pos.p, sizeof(unsigned) * 4, hipMemcpyDeviceToHost));
+    return GA_OK;
+}
+
+// which walk the last traceback ran: 0 the walk of stored words, 1 the recompute walk of traceback words, 2 the
+// tie-to-tie recompute walk (jump entries)
+int ga_debug_walk_kind(ga_ctx* c, int32_t* out) {
+    if (!c || !out) return fail(GA_E_ARG, "null argument");
+    out[0] = c->rc_used ? (c->rc_jump ? 2 : 1) : 0;
     return GA_OK;
 }
 

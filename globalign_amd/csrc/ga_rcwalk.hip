@@ -22,6 +22,7 @@
 #include "ga_lane.h"
 #include "ga_sync.h"
 #include "ga_walk.h"
+#include "ga_jump.h"
 
 namespace ga {
 
@@ -180,15 +181,242 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     }
 }
 
-template <int TD, int CB>
+// ---------------------------------------------------------------------------------------------------------------
+// The tie-to-tie walk's workers (ga_jump.h): the same recompute, but instead of traceback codes each
+// cell's three jump entries (one per entering level), built in the same skewed order as the cells themselves: the
+// entry of (r, c, L) is the cell's singleton move at level L prepended to the entry of the successor it moves to,
+// (r-1, c-1) at level 0, (r, c-1) at level 1 or (r-1, c) at level 2, which are exactly the cells the recurrence
+// reads (the diagonal and the left column come from lane l-1 by the same two DPP shifts as H' and h1').  A tie,
+// or a successor outside the block (the stripe's left edge, the block's first checkpoint row), ends the run.
+//
+// Per cell: an index from the saturated differences X'-H', Y'-H' (<= o+1, so o <= 14), M' != H' and a_i != b_j,
+// one 16-byte LUT read {selectors of (E0, E1), selector of E2, tie words of levels 0/1, of level 2}, three
+// prepends (one v_lshl_or each), two v_perm that pick each level's candidate (diag / left / up / none), and the
+// tie words or'ed in for the stored copy.
+constexpr int JSTAGE_ROWS = 65;  // the block's 64 rows + a scratch row for lanes outside them
+__host__ __device__ inline int rc_jump_worker_bytes(int TD, int every) {
+    return 3 * JSTAGE_ROWS * 64 * TD * 2 + rc_aw(every) * 4 + rc_aw(every) * 8;
+}
+constexpr int JLUT_OFF = 2048;                 // after the int16 sub' table
+constexpr int JWORK_OFF = JLUT_OFF + 1024 * 16;  // then the workers
+
+// LUT entry for index fx | fy << 4 | (M' != H') << 8 | (a != b) << 9 (fx, fy: X'-H', Y'-H' saturated at o+1):
+// the rank sets as ga_walk.h sets_from_code derives them, per level the v_perm selector of its candidate
+// (bytes 4,5 of {src0, Pu} = Pd (diag), 6,7 = Pl (left), 0,1 = Pu (up), 0x0c = zero for a tie) and its tie word
+__device__ inline uint4 jump_lut_entry(unsigned idx, int o) {
+    const unsigned fx = idx & 15u, fy = (idx >> 4) & 15u, zM = ((idx >> 8) & 1u) ^ 1u, mm = (idx >> 9) & 1u;
+    const unsigned uo = (unsigned)o;
+    const unsigned zX = fx == 0, zY = fy == 0, leX = fx <= uo, geX = fx >= uo, leY = fy <= uo, geY = fy >= uo;
+    const unsigned S[3] = {zM | (zX << 1) | (zY << 2), (zM & geX) | (leX << 1) | ((zY & geX) << 2),
+                           (zM & geY) | ((zX & geY) << 1) | (leY << 2)};
+    unsigned sel[3], tw[3];
+    for (int L = 0; L < 3; L++) {
+        const unsigned x = S[L];
+        if (x == 1u) { sel[L] = 0x0504u; tw[L] = 0; }
+        else if (x == 2u) { sel[L] = 0x0706u; tw[L] = 0; }
+        else if (x == 4u) { sel[L] = 0x0100u; tw[L] = 0; }
+        else { sel[L] = 0x0c0cu; tw[L] = x ? ((2u * x - 2u + 14u * mm) << 2) : 0x7cu; }  // (an empty set: never walked)
+    }
+    return make_uint4(sel[0] | (sel[1] << 16), sel[2] | (0x0c0cu << 16), tw[0] | (tw[1] << 16), tw[2]);
+}
+
+template <int TD>
+__device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4* lut, uint8_t* wl, int bi, int bs,
+                              int lane) {
+    static_assert(TD == 1 || TD == 2 || TD == 4, "jump entries: at most 4 columns per lane");
+    const int AW = rc_aw(r.stck_every);
+    constexpr int SC = 64 * TD;                                         // stage columns
+    uint16_t* stage = reinterpret_cast<uint16_t*>(wl);                  // [3][JSTAGE_ROWS][SC]
+    uint32_t* awin = reinterpret_cast<uint32_t*>(wl + 3 * JSTAGE_ROWS * SC * 2);
+    int2* ewin = reinterpret_cast<int2*>(awin + AW);
+    const int m = r.m, n = r.n, o = r.o;
+    const int R0 = bi * RC_ROWS;
+    const int nrow = min(RC_ROWS, m - R0);
+    const int ck = R0 / r.stck_every;
+    const int t0 = ck * r.stck_every;
+    const int nst = ((R0 + nrow + 62) - t0 + 1 + 7) & ~7;
+    const int base = t0 - 63;
+    const int s = bs;
+    const int j0 = s * 64 * TD, jl = j0 + lane * TD;
+    for (int i = lane; i < nst + 72; i += 64) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int x = base + i + u;
+            v |= (x >= 0 && x < m) ? (uint32_t)r.a[x] << (8 * u) : 0u;
+        }
+        awin[i] = v;
+    }
+    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
+    for (int i = lane; i < nst + 8; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
+    int bcode[TD];
+    int H[TD], Y[TD];
+    int Xl = 0, HLp = 0;
+#pragma unroll
+    for (int c = 0; c < TD; c++) bcode[c] = jl + c + 1 <= n ? r.b[jl + c] : 0;
+    if (ck == 0) {
+#pragma unroll
+        for (int c = 0; c < TD; c++) {
+            const int2 t = r.top[min(jl + c + 1, n)];
+            H[c] = t.x;
+            Y[c] = t.y;
+        }
+        HLp = r.top[min(jl, n)].x;
+    } else {
+        const int2* st = r.stck + ((long long)(ck - 1) * r.nstripes + s) * (TD + 1) * 64 + lane;
+#pragma unroll
+        for (int c = 0; c < TD; c++) {
+            const int2 v = st[c * 64];
+            H[c] = v.x;
+            Y[c] = v.y;
+        }
+        const int2 v = st[TD * 64];
+        Xl = v.x;
+        HLp = v.y;
+    }
+    int Hl = H[TD - 1];
+    const unsigned op1 = (unsigned)o + 1u;
+    // jump entries (as successors: a tie or a cell outside the block counts 0) of the previous step per column
+    int E0p[TD], E2p[TD];
+#pragma unroll
+    for (int c = 0; c < TD; c++) E0p[c] = E2p[c] = 0;
+    int E1last = 0, E0last = 0, E0dgn = 0;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    auto reads = [&](int g, int (&sb)[4][TD], int (&eh)[4], int (&ex)[4]) {
+        const uint32_t aw = awin[t0 + g - lane - base];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int ac = (int)((aw >> (8 * u)) & 0xffu) * 32;
+#pragma unroll
+            for (int c = 0; c < TD; c++) sb[u][c] = stab[ac + bcode[c]];
+        }
+        const int4 e01 = *reinterpret_cast<const int4*>(ewin + g);
+        const int4 e23 = *reinterpret_cast<const int4*>(ewin + g + 2);
+        eh[0] = e01.x; eh[1] = e01.z; eh[2] = e23.x; eh[3] = e23.z;
+        ex[0] = e01.y; ex[1] = e01.w; ex[2] = e23.y; ex[3] = e23.w;
+    };
+    auto group = [&](int g, const int (&sb)[4][TD], const int (&eh)[4], const int (&ex)[4], auto MK) {
+        constexpr bool MASKED = decltype(MK)::value;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int row = t0 + g + u - lane + 1;
+            const bool act = !MASKED || row >= 1;
+            int X = __builtin_amdgcn_update_dpp(ex[u], Xl, 0x138, 0xf, 0xf, false);
+            const int HLn = __builtin_amdgcn_update_dpp(eh[u], Hl, 0x138, 0xf, 0xf, false);
+            // the left lane's last-column entries: E1 of this row (its step t-1), E0 of the row above (t-2)
+            int El = __builtin_amdgcn_update_dpp(0, E1last, 0x138, 0xf, 0xf, false);
+            int Ed = E0dgn;
+            E0dgn = __builtin_amdgcn_update_dpp(0, E0last, 0x138, 0xf, 0xf, false);
+            int Hd = HLp;
+            // the block's rows go to the stage, the others to its scratch row
+            const unsigned rel = (unsigned)(row - R0 - 1);
+            uint16_t* dst = stage + (rel < 64u ? rel : 64u) * SC + lane * TD;
+            unsigned S01[TD], S2[TD];
+#pragma unroll
+            for (int c = 0; c < TD; c++) {
+                const int sw = sb[u][c];
+                const int M = Hd + (int)(int8_t)(sw & 0xff);
+                const int Hn = min(min(M, X), Y[c]);
+                unsigned idx = min((unsigned)(X - Hn), op1) | (min((unsigned)(Y[c] - Hn), op1) << 4) |
+                               (min((unsigned)(M - Hn), 1u) << 8);
+                idx |= (unsigned)sw & 0x200u;  // a_i != b_j (bit 9 of the sub' table entry)
+                const uint4 f = lut[idx];
+                const unsigned Pd = ((unsigned)Ed << 2) | 3u, Pl = ((unsigned)El << 2) | 1u,
+                               Pu = ((unsigned)E2p[c] << 2) | 2u;
+                const unsigned src0 = __builtin_amdgcn_perm(Pl, Pd, 0x05040100u);
+                const unsigned E01 = __builtin_amdgcn_perm(src0, Pu, f.x);
+                const unsigned E2v = __builtin_amdgcn_perm(src0, Pu, f.y);
+                S01[c] = E01 | f.z;
+                S2[c] = E2v | f.w;
+                Ed = E0p[c];
+                El = (int)(E01 >> 16);
+                E0p[c] = act ? (int)(E01 & 0xffffu) : E0p[c];
+                E2p[c] = act ? (int)E2v : E2p[c];
+                const int Ho = Hn + o;
+                X = min(X, Ho);
+                Y[c] = act ? min(Y[c], Ho) : Y[c];
+                Hd = H[c];
+                H[c] = act ? Hn : H[c];
+            }
+            E1last = act ? El : 0;
+            E0last = E0p[TD - 1];
+            Xl = X;
+            Hl = H[TD - 1];
+            HLp = HLn;
+            // the three levels' stored entries of this row's TD columns
+            if constexpr (TD == 4) {
+                typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                const u2v w0 = {__builtin_amdgcn_perm(S01[1], S01[0], 0x05040100u), __builtin_amdgcn_perm(S01[3], S01[2], 0x05040100u)};
+                const u2v w1 = {__builtin_amdgcn_perm(S01[1], S01[0], 0x07060302u), __builtin_amdgcn_perm(S01[3], S01[2], 0x07060302u)};
+                const u2v w2 = {__builtin_amdgcn_perm(S2[1], S2[0], 0x05040100u), __builtin_amdgcn_perm(S2[3], S2[2], 0x05040100u)};
+                *reinterpret_cast<u2v*>(dst) = w0;
+                *reinterpret_cast<u2v*>(dst + JSTAGE_ROWS * SC) = w1;
+                *reinterpret_cast<u2v*>(dst + 2 * JSTAGE_ROWS * SC) = w2;
+            } else if constexpr (TD == 2) {
+                *reinterpret_cast<unsigned*>(dst) = __builtin_amdgcn_perm(S01[1], S01[0], 0x05040100u);
+                *reinterpret_cast<unsigned*>(dst + JSTAGE_ROWS * SC) = __builtin_amdgcn_perm(S01[1], S01[0], 0x07060302u);
+                *reinterpret_cast<unsigned*>(dst + 2 * JSTAGE_ROWS * SC) = __builtin_amdgcn_perm(S2[1], S2[0], 0x05040100u);
+            } else {
+                dst[0] = (uint16_t)S01[0];
+                dst[JSTAGE_ROWS * SC] = (uint16_t)(S01[0] >> 16);
+                dst[2 * JSTAGE_ROWS * SC] = (uint16_t)S2[0];
+            }
+        }
+    };
+    int sbA[4][TD], ehA[4], exA[4], sbB[4][TD], ehB[4], exB[4];
+    reads(0, sbA, ehA, exA);
+    const int gmask = ck == 0 ? 64 : 0;
+    for (int g = 0; g < nst; g += 8) {
+        reads(g + 4, sbB, ehB, exB);
+        if (g < gmask) group(g, sbA, ehA, exA, std::true_type{});
+        else group(g, sbA, ehA, exA, std::false_type{});
+        reads(g + 8, sbA, ehA, exA);
+        if (g + 4 < gmask) group(g + 4, sbB, ehB, exB, std::true_type{});
+        else group(g + 4, sbB, ehB, exB, std::false_type{});
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    {
+        // (the reach check of rc_block: a block the walker can no longer reach is not written)
+        const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
+        const int tile = pv ? (int)(pv - 1u) : r.tile0;
+        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return;
+    }
+    // the block's 2 x 2TD tiles of 32 x 32 cells, 6 KB each ([level][32 rows][32 columns], ga_jump.h), into its
+    // cache slot with write-through stores
+    uint8_t* blk = r.tb + (size_t)((bi % RC_CACHE_I) * RC_CACHE_S + bs % RC_CACHE_S) * (4 * TD * JTILE_BYTES);
+#pragma unroll
+    for (int tr = 0; tr < 2; tr++)
+#pragma unroll
+        for (int tc = 0; tc < 2 * TD; tc++) {
+            uint4* dst = reinterpret_cast<uint4*>(blk + (tr * 2 * TD + tc) * JTILE_BYTES) + lane;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                const int p = q >> 1, row = tr * 32 + (q & 1) * 16 + (lane >> 2), col = tc * 32 + (lane & 3) * 8;
+                const uint4 v = *reinterpret_cast<const uint4*>(stage + (p * JSTAGE_ROWS + row) * SC + col);
+                st16_sc1(dst + q * 64, v);
+            }
+        }
+}
+
+template <int TD, int CB, bool JUMP = false>
 __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     const int lane = threadIdx.x & 63;
     const int wave = sgpr((int)(threadIdx.x >> 6));
     int8_t* stab = reinterpret_cast<int8_t*>(dyn);  // [K][32] sub'
-    for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x) stab[(q / r.K) * 32 + q % r.K] = (int8_t)r.subp[q];
+    int16_t* stab16 = reinterpret_cast<int16_t*>(dyn);  // JUMP: [K][32] sub' | (a != b) << 9
+    uint4* lut = reinterpret_cast<uint4*>(dyn + JLUT_OFF);
+    if constexpr (JUMP) {
+        for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x)
+            stab16[(q / r.K) * 32 + q % r.K] = (int16_t)((r.subp[q] & 0xff) | (q / r.K != q % r.K ? 0x200 : 0));
+        for (int q = threadIdx.x; q < 1024; q += blockDim.x) lut[q] = jump_lut_entry((unsigned)q, r.o);
+    } else {
+        for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x) stab[(q / r.K) * 32 + q % r.K] = (int8_t)r.subp[q];
+    }
     __syncthreads();
     if (wave >= r.workers) return;
-    uint8_t* wl = dyn + 1024 + wave * r.worker_bytes;
+    uint8_t* wl = dyn + (JUMP ? JWORK_OFF : 1024) + wave * r.worker_bytes;
     const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
     const int dbi = r.off[lane] >> 4, dbs = r.off[lane] & 15;
     unsigned idle = 0;
@@ -214,7 +442,8 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
                                                            __ATOMIC_RELAXED, __ATOMIC_RELAXED, AGENT);
             if (sgpr(won)) {
                 const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-                rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
+                if constexpr (JUMP) rc_block_jump<TD>(r, stab16, lut, wl, bi_i, bs_i, lane);
+                else rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the flag
                 if (lane == 0) g_st(r.flags + (long long)bi_i * r.nbs + bs_i, ready);
                 if (lane == 0) {  // diagnostics: blocks recomputed, their total time (100 MHz ticks)
@@ -239,6 +468,33 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_rc_kernel(WalkArgs w, Rc
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
     if (blockIdx.x == 0) walk_body<CB, true>(w, w.rng, reinterpret_cast<uint16_t*>(dyn));
     else rc_server<TD, CB>(r, dyn);
+}
+
+// the tie-to-tie walk: workgroup 0 walks with jump entries, the others build them
+template <int TD>
+__global__ void __launch_bounds__(64 * JWALK_WAVES) walk_rc_jump_kernel(WalkArgs w, RcArgs r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    if (blockIdx.x == 0) walk_jump_body(w, w.rng, reinterpret_cast<uint16_t*>(dyn));
+    else rc_server<TD, 1, true>(r, dyn);
+}
+
+template <int TD>
+static void launch_rc_jump_one(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {
+    const size_t lds = std::max<size_t>(jump_torus_bytes(), (size_t)JWORK_OFF + (size_t)r.workers * r.worker_bytes);
+    auto* fn = walk_rc_jump_kernel<TD>;
+    (void)hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    fn<<<dim3(1 + nserv), dim3(64 * JWALK_WAVES), lds, s>>>(w, r);
+}
+
+int rc_jump_worker_bytes_host(int TD, int every) { return rc_jump_worker_bytes(TD, every); }
+size_t rc_jump_lds_bytes(int TD, int every) { return (size_t)JWORK_OFF + (size_t)rc_jump_worker_bytes(TD, every); }
+
+void launch_walk_rc_jump(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {
+    switch (r.TD) {
+        case 1: launch_rc_jump_one<1>(s, w, r, nserv); break;
+        case 2: launch_rc_jump_one<2>(s, w, r, nserv); break;
+        default: launch_rc_jump_one<4>(s, w, r, nserv); break;
+    }
 }
 
 template <int CB, int TD>

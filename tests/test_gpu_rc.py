@@ -4,6 +4,7 @@ walks while recompute workgroups rebuild the traceback words of the 64-row block
 must equal the single-problem oracle exactly: cost, the three alignment strings, the final random state.
 GA_RC=1 forces the path at small sizes; the full-size C3 pin takes it by default
 (test_gpu_parity.py::test_bench_workload_cost_matches_golden)."""
+import os
 import random
 
 import numpy as np
@@ -14,6 +15,7 @@ from tests.conftest import splitmix_seq
 pytestmark = pytest.mark.gpu
 
 DNA = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+JUMP_DEFAULT = "0"  # ga_host.cpp kRcJumpDefault
 
 
 def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
@@ -36,9 +38,13 @@ def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
         eng.load(tables.codes(a1), tables.codes(a2), tables)
         cost, strings, status, mt_after = eng.align(mt, a1, a2)
         kind = eng.fill_kind()
+        walk = eng.walk_kind()
     finally:
         eng.close()
     assert kind[0] == "rc", kind  # the recompute path really ran
+    # the tie-to-tie walk (jump entries) wherever its workers fit: <= 4 columns per lane, o <= 14
+    jump_ok = kind[1] <= 4 and goc <= 14 and str((env or {}).get("GA_RC_JUMP", os.environ.get("GA_RC_JUMP", JUMP_DEFAULT))) != "0"
+    assert walk == ("jump" if jump_ok else "rc"), (walk, kind, goc)
     assert status == 0
     assert int(cost) == ref["cost"]
     assert tuple(strings) == tuple(ref["strings"])
@@ -234,3 +240,20 @@ def test_small_device_memory_bands(monkeypatch):
     """With little free device memory (GA_DEV_AVAIL_MB caps what the sizing sees) the recompute walk declines and
     the traceback words are banded to fit, instead of a stored-words fill that cannot allocate."""
     _align_fallback(monkeypatch, {"GA_DEV_AVAIL_MB": 1}, seed=2)
+
+
+@pytest.mark.parametrize("jump", [0, 1])
+@pytest.mark.parametrize("m,n,seed", [(3000, 2600, 71), (2049, 4100, 72)])
+def test_rc_jump_and_word_walks_vs_oracle(monkeypatch, jump, m, n, seed):
+    """Both recompute walks on the same problems: the tie-to-tie walk (jump entries) and the walk of
+    recomputed traceback words (GA_RC_JUMP=0)."""
+    _align(monkeypatch, splitmix_seq(m, seed, "dna"), splitmix_seq(n, seed + 1, "dna"), DNA, seed=seed,
+           env={"GA_RC_JUMP": jump})
+
+
+@pytest.mark.parametrize("o", [1, 2, 6, 14])
+def test_rc_jump_gap_opens_vs_oracle(monkeypatch, o):
+    """Gap opens across the jump LUT's range (X'-H', Y'-H' saturated at o+1 <= 15), incl. o = 1 and the largest, 14."""
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-o, gap_extension_score=-1)
+    _align(monkeypatch, splitmix_seq(1800, 81 + o, "dna"), splitmix_seq(1900, 82 + o, "dna"), kw, seed=o,
+           env={"GA_RC_JUMP": 1})

@@ -87,6 +87,16 @@ __global__ void trips(const uint16_t* img, const uint32_t* tabimg, long long* ou
     sink[lane] = acc + roff + coff + (unsigned)L;
 }
 
+// v_perm_b32 semantics check (the jump build selects 16-bit candidates with it): byte k of the result is byte
+// sel_k of {a, b} (b = bytes 0..3, a = bytes 4..7), 0x0c gives 0x00
+__global__ void perm_check(unsigned* out) {
+    const unsigned a = 0x77665544u, b = 0x33221100u;
+    out[0] = __builtin_amdgcn_perm(a, b, 0x05040100u);
+    out[1] = __builtin_amdgcn_perm(a, b, 0x0c0c0706u);
+    out[2] = __builtin_amdgcn_perm(a, b, 0x03020c0cu);
+    out[3] = __builtin_amdgcn_perm(a, b, 0x0d0d0b0au);
+}
+
 static unsigned rnd(unsigned long long& s) {
     s = s * 6364136223846793005ull + 1442695040888963407ull;
     return (unsigned)(s >> 33);
@@ -138,6 +148,15 @@ int main() {
     (void)hipMalloc(&dtab, tab.size() * 4);
     (void)hipMemcpy(dimg, img.data(), img.size() * 2, hipMemcpyHostToDevice);
     (void)hipMemcpy(dtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+    {
+        unsigned* d;
+        unsigned h[4];
+        (void)hipMalloc(&d, 16);
+        perm_check<<<1, 64>>>(d);
+        (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+        printf("perm: %08x %08x %08x %08x (expect 55441100 00007766 33220000 ...)\n", h[0], h[1], h[2], h[3]);
+        (void)hipFree(d);
+    }
     run("trip, tie move in SALU", trips<0>, dimg, dtab);
     run("trip, tie move in VALU", trips<1>, dimg, dtab);
     return 0;
