@@ -129,6 +129,7 @@ struct RcArgs {
     unsigned spin_limit;   // idle polls before a worker gives up (the walk then reports its own timeout)
     int nwin;              // window blocks (<= 64)
     unsigned char off[64]; // window offsets (dbi << 4 | dbs) from the walker's block, likeliest first
+    const uint4* jlut;     // the tie-to-tie walk's worker LUT (1024 entries, jump_lut_build), or nullptr
 };
 
 // Pipelined walks in one launch (walk_chain_kernel): walk k uses w[k % S] with rng = tab + G_k.
@@ -159,6 +160,10 @@ int rc_worker_bytes(int TD, int CB, int stck_every);
 void launch_walk_rc_jump(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv);
 int rc_jump_worker_bytes_host(int TD, int stck_every);
 size_t rc_jump_lds_bytes(int TD, int stck_every);  // LDS of a workgroup with one jump worker
+// The jump workers' LUT (host, ga_host.cpp): entry idx = fx | fy << 4 | (M' != H') << 8 | (a != b) << 9, fx / fy the
+// cell's X'-H' / Y'-H' saturated at o+1 (o <= 14): {v_perm selectors of levels 0 | 1 << 16, of level 2 (high half
+// 0x0c0c), tie words of levels 0 | 1 << 16, of level 2}
+void jump_lut_build(int o, uint32_t* out4096);
 // traceback words of a caller-supplied (m+1) x (n+1) x 3 cell array (dp_array_backward shim)
 void launch_tb_from_cells(hipStream_t s, const int* cells, int m, int n, int o, int CB, int TC, uint8_t* tb);
 // score-only anti-diagonal fill (64-column stripes; FillArgs.cols_per_lane must be 1)

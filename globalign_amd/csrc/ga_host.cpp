@@ -406,6 +406,9 @@ struct ga_ctx {
     DevBuf dbg, wdbg;
     // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
     DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
+    int walk_jump_diag[3] = {0, 0, 0};  // the tie-to-tie walk's trips, region re-checks, ties (result[12..14])
+    DevBuf jlut;           // the jump workers' LUT for gap open jlut_o (ga::jump_lut_build)
+    int jlut_o = -1;
     // ga_slab_link: this slab's left edge + its progress word, uncached device memory on this GPU that
     // the left neighbour's fill writes (over xGMI when it runs on another GPU)
     DevBuf link;
@@ -1086,6 +1089,7 @@ int decode_segment(ga_ctx* c, const int* res, WalkStart& st, int& reason, const 
     c->walk_c_total = res[9];
     c->walk_load_ticks = res[10];
     c->walk_load_count = res[11];
+    for (int q = 0; q < 3; q++) c->walk_jump_diag[q] = res[12 + q];
     if (!synced) HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
     const int64_t D0 = st.D, D1 = res[0];
     reason = res[3];
@@ -1367,6 +1371,17 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     if (const char* e = c->knob("GA_RC_WPW")) r.workers = std::max(1, std::min(r.workers, atoi(e)));
     else r.workers = 1;
     r.spin_limit = 1u << 20;
+    r.jlut = nullptr;
+    if (c->rc_jump) {
+        if (c->jlut_o != c->o) {
+            std::vector<uint32_t> lut(4096);
+            ga::jump_lut_build(c->o, lut.data());
+            HIPCHK(c->jlut.ensure(sizeof(uint32_t) * lut.size()));
+            HIPCHK(hipMemcpy(c->jlut.p, lut.data(), sizeof(uint32_t) * lut.size(), hipMemcpyHostToDevice));
+            c->jlut_o = c->o;
+        }
+        r.jlut = c->jlut.as<uint4>();
+    }
     {
         // the window: blocks up-left of the walker's (dbi block rows, dbs stripes), the path's likeliest
         // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
@@ -1516,6 +1531,7 @@ int streamed_walk_finish(ga_ctx* c, const RngTable& R, const WalkBufs& wb, const
         c->walk_c_total = res[9];
         c->walk_load_ticks = res[10];
         c->walk_load_count = res[11];
+        for (int q = 0; q < 3; q++) c->walk_jump_diag[q] = res[12 + q];
         reason = res[3];
         if (reason == 7) return fail(GA_E_TIMEOUT, "recompute walk: a tile was never recomputed");
         const int64_t D1 = res[0];
@@ -2747,11 +2763,33 @@ int ga_debug_rc(ga_ctx* c, unsigned* out4) {
     return GA_OK;
 }
 
+// diagnostics / CPU tests: the jump workers' LUT for gap open o (4096 words)
+int ga_debug_jump_lut(int32_t o, uint32_t* out4096) {
+    if (!out4096 || o < 0 || o > 14) return fail(GA_E_ARG, "bad argument");
+    ga::jump_lut_build(o, out4096);
+    return GA_OK;
+}
+
+// diagnostics: the recompute walk's tile / entry cache (rc_tb) as the last walk left it
+int ga_debug_rc_cache(ga_ctx* c, void* out, int64_t bytes) {
+    if (!c || !out) return fail(GA_E_ARG, "null argument");
+    if (!c->rc_tb.p) return fail(GA_E_STATE, "no recompute walk ran");
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, c->rc_tb.p, std::min<size_t>((size_t)bytes, c->rc_tb.cap), hipMemcpyDeviceToHost));
+    return GA_OK;
+}
+
 // which walk the last traceback ran: 0 the walk of stored words, 1 the recompute walk of traceback words, 2 the
 // tie-to-tie recompute walk (jump entries)
 int ga_debug_walk_kind(ga_ctx* c, int32_t* out) {
     if (!c || !out) return fail(GA_E_ARG, "null argument");
     out[0] = c->rc_used ? (c->rc_jump ? 2 : 1) : 0;
+    return GA_OK;
+}
+
+int ga_debug_walk_jump(ga_ctx* c, int* out3) {
+    if (!c || !out3) return fail(GA_E_ARG, "null argument");
+    for (int q = 0; q < 3; q++) out3[q] = c->walk_jump_diag[q];
     return GA_OK;
 }
 
@@ -2778,3 +2816,28 @@ int ga_last_timings(ga_ctx* c, float* out4) {
 }
 
 }  // extern "C"
+
+namespace ga {
+// The rank sets of a cell from its saturated differences (as ga_walk.h sets_from_code): per level the v_perm
+// selector of the candidate its singleton move takes (bytes 4,5 of {src0, Pu} = Pd (diag), 6,7 = Pl (left), 0,1 = Pu
+// (up)) or 0x0c0c (a zero half) for a tie, and the tie word ((2S - 2 + 14*(a != b)) << 2) the walker reads at a tie
+void jump_lut_build(int o, uint32_t* out) {
+    const unsigned uo = (unsigned)o;
+    for (unsigned idx = 0; idx < 1024; idx++) {
+        const unsigned fx = idx & 15u, fy = (idx >> 4) & 15u, zM = ((idx >> 8) & 1u) ^ 1u, mm = (idx >> 9) & 1u;
+        const unsigned zX = fx == 0, zY = fy == 0, leX = fx <= uo, geX = fx >= uo, leY = fy <= uo, geY = fy >= uo;
+        const unsigned S[3] = {zM | (zX << 1) | (zY << 2), (zM & geX) | (leX << 1) | ((zY & geX) << 2),
+                               (zM & geY) | ((zX & geY) << 1) | (leY << 2)};
+        unsigned sel[3], tw[3];
+        for (int L = 0; L < 3; L++) {
+            const unsigned x = S[L];
+            sel[L] = x == 1u ? 0x0504u : x == 2u ? 0x0706u : x == 4u ? 0x0100u : 0x0c0cu;
+            tw[L] = (x == 1u || x == 2u || x == 4u) ? 0u : x ? ((2u * x - 2u + 14u * mm) << 2) : 0x7cu;  // (empty: never walked)
+        }
+        out[4 * idx] = sel[0] | (sel[1] << 16);
+        out[4 * idx + 1] = sel[2] | (0x0c0cu << 16);
+        out[4 * idx + 2] = tw[0] | (tw[1] << 16);
+        out[4 * idx + 3] = tw[2];
+    }
+}
+}  // namespace ga

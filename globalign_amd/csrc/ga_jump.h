@@ -220,6 +220,7 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
     const int jend = w.handoff ? 5 : 2;  // reason when the walk reaches local column 0
     const int iend = 1;
     int cti = -1, ctj = -1, nwait = 0, ntiles = 0;
+    int ntrips = 0, nverify = 0, nties = 0;  // diagnostics (result[12..14])
     unsigned rc_spins = 0;
     bool rc_degenerate = false;
     const int maxh = w.maxh;
@@ -353,42 +354,72 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
         const unsigned plane = 2u * JPLANE * (unsigned)(lane < 3 ? lane : lane < 6 ? lane - 3 : 0);
         const unsigned ebase = lds_addr(E) + plane;
         const unsigned tbase = lds_addr(jrngbuf);
-        for (;;) {
-            // a trip from (i, j) reads rows / columns down to i - 1, j - 1 and lands at most 9 above / left:
-            // inside the verified tiles while i - 10 >= vlo_i and j - 10 >= vlo_j.  Re-verified at the walk's
-            // tile; still short of that means the walk is within 10 of row / column 1 (vlo = 1): per step then
-            if (__builtin_expect(i - 10 < vlo_i || j - 10 < vlo_j, 0)) {
-                verify(i, j);
-                if (i - 10 < vlo_i || j - 10 < vlo_j) break;
-            }
-            // the fetch
+        // One trip: t's entries and its successors' (lanes 0..5) and the table entry of dispatch D, one LDS round
+        // trip.  The loop is software-pipelined so that only the chain sits between a fetch landing and the next
+        // fetch going out: the entry taken (readlane), the advance (i, j: a mask and a bit count each), the next
+        // fetch's addresses; the level record (put), the move count and the region check run while it is in flight.
+        // A fetch whose cell has left the verified tiles reads harmless torus cells (the addresses are masked): the
+        // check after it then re-verifies and fetches again.
+        auto fetch_e = [&](unsigned& v) {  // the entries: needs only (i, j)
             const unsigned roff = ((unsigned)(i - 1) & (JP - 1)) << 8, coff = ((unsigned)(j - 1) & (JP - 1)) << 1;
             const unsigned addr = ebase + (((roff - drow) & (2u * JP * (JP - 1))) | ((coff - dcol) & (2u * (JP - 1))));
-            unsigned v, tb;
             asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(addr));
-            asm volatile("ds_read_b32 %0, %1" : "=v"(tb) : "v"(tbase + (((unsigned)D & (RB - 1)) << 2)));
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(tb));
-            const unsigned e = (unsigned)__builtin_amdgcn_readlane((int)v, L);
-            unsigned W;
-            if (e & 3u) {
-                W = e;
-            } else {
-                // a tie: the table picks the level x; W = the tie move, then x's successor's run (none if a tie)
-                const unsigned t = (unsigned)__builtin_amdgcn_readfirstlane((int)tb);
-                const unsigned x = (t >> (((e >> 2) & 31u) + 3u)) & 3u;
-                const unsigned s = (unsigned)__builtin_amdgcn_readlane((int)v, (int)(3u + x));
-                W = (((s & 3u) ? s : 0u) << 2) | jcode(x);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto fetch_t = [&](unsigned& tb, int d) {  // the table entry of dispatch d
+            asm volatile("ds_read_b32 %0, %1" : "=v"(tb) : "v"(tbase + (((unsigned)d & (RB - 1)) << 2)));
+        };
+        auto outside = [&]() { return ((i - 10 - vlo_i) | (j - 10 - vlo_j)) < 0; };
+        verify(i, j);
+        if (!outside()) {
+            unsigned v, tb;
+            fetch_e(v);
+            fetch_t(tb, D);
+            for (;;) {
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(tb));
+                const unsigned e = (unsigned)__builtin_amdgcn_readlane((int)v, L);
+                unsigned W;
+                ntrips++;
+                if (__builtin_expect(e & 3u, 1)) {
+                    W = e;
+                } else {
+                    nties++;
+                    // a tie: the table picks the level x; W = the tie move, then x's successor's run (none if a tie)
+                    const unsigned t = (unsigned)__builtin_amdgcn_readfirstlane((int)tb);
+                    const unsigned x = (t >> (((e >> 2) & 31u) + 3u)) & 3u;
+                    const unsigned sx = (unsigned)__builtin_amdgcn_readlane((int)v, (int)(3u + x));
+                    W = (((sx & 3u) ? sx : 0u) << 2) | jcode(x);
+                }
+                // the table entry first, then the entries (they land in issue order: the wait at the top of the
+                // loop is then the entries' own)
+                const int k = __builtin_popcount((W | (W >> 1)) & 0x55555u);
+                fetch_t(tb, D + k);
+                i -= __builtin_popcount(W & 0xaaaaau);
+                j -= __builtin_popcount(W & 0x55555u);
+                fetch_e(v);  // speculative while the region check below is pending
+                if (__builtin_expect(((D + k) ^ D) >> 9, 0)) {
+                    // a new block of table entries: the helper keeps the ring 3 blocks ahead, but make sure (and read
+                    // the entry again once it is there)
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(tb));
+                    rng_ready(D + k);
+                    fetch_t(tb, D + k);
+                }
+                L = (int)jlevel((W >> (2 * k - 2)) & 3u);
+                // the moves as levels, MSB first: bit-reversing W swaps each field's two bits, and xor 3 maps the
+                // swapped codes (diag 3, left 2, up 1) to the levels 0, 1, 2
+                put(__builtin_bitreverse32(W) ^ ~(0xffffffffu >> (2 * k)), k);
+                h += k;
+                if (__builtin_expect(outside(), 0)) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(tb));
+                    nverify++;
+                    verify(i, j);
+                    if (outside()) break;
+                    fetch_e(v);
+                    fetch_t(tb, D);
+                }
             }
-            const int k = __builtin_popcount((W | (W >> 1)) & 0x55555u);
-            i -= __builtin_popcount(W & 0xaaaaau);
-            j -= __builtin_popcount(W & 0x55555u);
-            L = (int)jlevel((W >> (2 * k - 2)) & 3u);
-            // the moves as levels, MSB first: bit-reversing W swaps each field's two bits, and xor 3 maps the
-            // swapped codes (diag 3, left 2, up 1) to the levels 0, 1, 2
-            put(__builtin_bitreverse32(W) ^ ~(0xffffffffu >> (2 * k)), k);
-            h += k;
-            if (first) first = 0;
         }
+        first = 0;
         // the last moves, per step, near row / column 0
         while (reason < 0 && !step()) {}
     }
@@ -403,6 +434,9 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
         w.result[9] = (int)((__builtin_amdgcn_s_memtime() - c_start) >> 4);
         w.result[10] = (int)jload_ticks;
         w.result[11] = jload_count;
+        w.result[12] = ntrips;
+        w.result[13] = nverify;
+        w.result[14] = nties;
         __hip_atomic_store(&jwD, D, __ATOMIC_RELEASE, WGS);
         __hip_atomic_store(&jwalk_done, 1, __ATOMIC_RELEASE, WGS);
     }

@@ -200,26 +200,6 @@ __host__ __device__ inline int rc_jump_worker_bytes(int TD, int every) {
 constexpr int JLUT_OFF = 2048;                 // after the int16 sub' table
 constexpr int JWORK_OFF = JLUT_OFF + 1024 * 16;  // then the workers
 
-// LUT entry for index fx | fy << 4 | (M' != H') << 8 | (a != b) << 9 (fx, fy: X'-H', Y'-H' saturated at o+1):
-// the rank sets as ga_walk.h sets_from_code derives them, per level the v_perm selector of its candidate
-// (bytes 4,5 of {src0, Pu} = Pd (diag), 6,7 = Pl (left), 0,1 = Pu (up), 0x0c = zero for a tie) and its tie word
-__device__ inline uint4 jump_lut_entry(unsigned idx, int o) {
-    const unsigned fx = idx & 15u, fy = (idx >> 4) & 15u, zM = ((idx >> 8) & 1u) ^ 1u, mm = (idx >> 9) & 1u;
-    const unsigned uo = (unsigned)o;
-    const unsigned zX = fx == 0, zY = fy == 0, leX = fx <= uo, geX = fx >= uo, leY = fy <= uo, geY = fy >= uo;
-    const unsigned S[3] = {zM | (zX << 1) | (zY << 2), (zM & geX) | (leX << 1) | ((zY & geX) << 2),
-                           (zM & geY) | ((zX & geY) << 1) | (leY << 2)};
-    unsigned sel[3], tw[3];
-    for (int L = 0; L < 3; L++) {
-        const unsigned x = S[L];
-        if (x == 1u) { sel[L] = 0x0504u; tw[L] = 0; }
-        else if (x == 2u) { sel[L] = 0x0706u; tw[L] = 0; }
-        else if (x == 4u) { sel[L] = 0x0100u; tw[L] = 0; }
-        else { sel[L] = 0x0c0cu; tw[L] = x ? ((2u * x - 2u + 14u * mm) << 2) : 0x7cu; }  // (an empty set: never walked)
-    }
-    return make_uint4(sel[0] | (sel[1] << 16), sel[2] | (0x0c0cu << 16), tw[0] | (tw[1] << 16), tw[2]);
-}
-
 template <int TD>
 __device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4* lut, uint8_t* wl, int bi, int bs,
                               int lane) {
@@ -410,7 +390,7 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     if constexpr (JUMP) {
         for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x)
             stab16[(q / r.K) * 32 + q % r.K] = (int16_t)((r.subp[q] & 0xff) | (q / r.K != q % r.K ? 0x200 : 0));
-        for (int q = threadIdx.x; q < 1024; q += blockDim.x) lut[q] = jump_lut_entry((unsigned)q, r.o);
+        for (int q = threadIdx.x; q < 1024; q += blockDim.x) lut[q] = r.jlut[q];  // built by the host (jump_lut_build)
     } else {
         for (int q = threadIdx.x; q < r.K * r.K; q += blockDim.x) stab[(q / r.K) * 32 + q % r.K] = (int8_t)r.subp[q];
     }

@@ -125,3 +125,40 @@ def test_engine_cache_keeps_one_knob_set(monkeypatch):
     del e0
     gc.collect()
     assert sum(r() is not None for r in made) == 4       # the current set's: 2 default + 2 slab engines
+
+
+def _perm(a, b, sel):
+    """v_perm_b32: byte k of the result is byte sel_k of {a, b} (b = bytes 0..3), 0x0c gives 0x00"""
+    src = [(b >> (8 * k)) & 0xff for k in range(4)] + [(a >> (8 * k)) & 0xff for k in range(4)]
+    return sum((src[s] if s < 8 else (0 if s == 12 else 0xff)) << (8 * k) for k, s in
+               enumerate((sel >> (8 * k)) & 0xff for k in range(4)))
+
+
+@pytest.mark.parametrize("o", [0, 1, 5, 10, 14])
+def test_jump_lut_selects_the_singleton_move(lib, o):
+    """The tie-to-tie walk's worker LUT (ga_host.cpp jump_lut_build): for every combination of
+    saturated differences its selectors pick, per entering level, the candidate of the level's unique minimum (diag
+    Pd / left Pl / up Pu) and a zero half plus the walk's tie word for a tie -- checked against the rank sets of the
+    reference's rank test (argmin of (M, X, Y), (M+o, X, Y+o), (M+o, X+o, Y); globaligner.py:431-441, :490-514)."""
+    lut = np.zeros(4096, dtype=np.uint32)
+    lib.ga_debug_jump_lut.argtypes = [C.c_int32, C.c_void_p]
+    assert lib.ga_debug_jump_lut(o, lut.ctypes.data) == 0
+    Pd, Pl, Pu = 0x1113, 0x2221, 0x3332  # distinct 16-bit candidates
+    src0 = _perm(Pl, Pd, 0x05040100)
+    for dM in range(0, 3):
+        for dX in range(0, o + 4):
+            for dY in range(0, o + 4):
+                if min(dM, dX, dY):
+                    continue
+                for mm in (0, 1):
+                    H = 100
+                    M, X, Y = H + dM, H + dX, H + dY
+                    idx = min(dX, o + 1) | (min(dY, o + 1) << 4) | (min(dM, 1) << 8) | (mm << 9)
+                    e01 = _perm(src0, Pu, int(lut[4 * idx])) | int(lut[4 * idx + 2])
+                    e2 = _perm(src0, Pu, int(lut[4 * idx + 1])) | int(lut[4 * idx + 3])
+                    got = (e01 & 0xffff, e01 >> 16, e2 & 0xffff)
+                    for L, vals in enumerate(((M, X, Y), (M + o, X, Y + o), (M + o, X + o, Y))):
+                        h = min(vals)
+                        S = sum(1 << k for k in range(3) if vals[k] == h)
+                        want = {1: Pd, 2: Pl, 4: Pu}.get(S, (2 * S - 2 + 14 * mm) << 2)
+                        assert got[L] == want, (o, dM, dX, dY, mm, L, hex(got[L]), hex(want))

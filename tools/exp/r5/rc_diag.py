@@ -20,6 +20,7 @@ tables, _ = bench.problem_tables(s1, s2)
 L = _native.load_library()
 L.ga_debug_walk.argtypes = [C.c_void_p, C.c_void_p]
 L.ga_debug_rc.argtypes = [C.c_void_p, C.c_void_p]
+L.ga_debug_walk_jump.argtypes = [C.c_void_p, C.c_void_p]
 mt0 = np.random.RandomState(0).randint(0, 2**32, size=625, dtype=np.uint64).astype(np.uint32)
 mt0[624] = 624
 os.environ["GA_RC"] = "1"
@@ -37,8 +38,11 @@ for cfg in cfgs:
         rc = np.zeros(4, dtype=np.uint32)
         L.ga_debug_rc(eng._h, rc.ctypes.data)
         steps = len(r[1][0])
+        jd = np.zeros(3, dtype=np.int32)
+        L.ga_debug_walk_jump(eng._h, jd.ctypes.data)
         print(f"steps={steps} ns_per_step={t['walk_ms'] * 1e6 / steps:.1f} servers={ns} win={win} fill={t['fill_ms']:.3f} "
               f"walk={t['walk_ms']:.3f} call={t['call_ms']:.3f} kind={eng.fill_kind()} waits={w[0]} tiles={w[1]} "
               f"t_tile_ms={w[2] / 1e5:.3f} t_total_ms={w[4] / 1e5:.3f} loads={w[7]} load_us_avg={w[6] / max(w[7], 1) / 100:.2f} "
-              f"| rc blocks={rc[2]} block_us_avg={rc[3] / max(rc[2], 1) / 100:.2f}", flush=True)
+              f"| rc blocks={rc[2]} block_us_avg={rc[3] / max(rc[2], 1) / 100:.2f} | jump trips={jd[0]} rechecks={jd[1]} ties={jd[2]} "
+              f"moves_per_trip={steps / max(jd[0], 1):.2f} walk_ns_per_trip_ex_waits={(w[4] - w[2]) * 10.0 / max(jd[0], 1):.1f}", flush=True)
     eng.close()
