@@ -97,12 +97,15 @@ struct WalkArgs {
 };
 
 // The recompute walk's tile cache: block (bi, bs) (64 rows of fill stripe bs) lives at slot
-// (bi mod RC_CACHE_I, bs mod RC_CACHE_S).  Candidates lie at most RC_SPAN_MAX - 1 = 15 block rows / stripes
-// up-left of the walker's block as a worker saw it, and the cache is twice that deep on both axes: a worker
-// whose view of the walker is stale can then never overwrite a block the walker may still read (the safety
-// argument at rc_block's cache store, ga_rcwalk.hip; ADVICE r3: with a 16-deep cache it could)
-constexpr int RC_SPAN_MAX = 16;
-constexpr int RC_CACHE_I = 32;
+// (bi mod RC_CACHE_I, bs mod RC_CACHE_S).  Candidates lie at most RC_SPAN_I - 1 = 31 block rows and RC_SPAN_S - 1
+// = 7 stripes up-left of the walker's block as a worker saw it (offsets dbi * 8 + dbs in a byte), and the cache is
+// twice that deep on both axes: a worker whose view of the walker is stale can then never overwrite a block the
+// walker may still read (the safety argument at rc_block's cache store, ga_rcwalk.hip; ADVICE r3: with a cache
+// only as deep as the candidates it could).  Deep along the rows, narrow across the stripes: a 64-row block is a
+// quarter of a TD 4 stripe's width, and the path runs near the diagonal.
+constexpr int RC_SPAN_I = 32;
+constexpr int RC_SPAN_S = 8;
+constexpr int RC_CACHE_I = 2 * RC_SPAN_I;
 constexpr int RC_CACHE_S = 32;
 
 // The recompute workgroups of walk_rc_kernel (ga_rcwalk.hip): each wave recomputes 64-row

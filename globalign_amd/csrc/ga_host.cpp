@@ -1385,31 +1385,35 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     {
         // the window: blocks up-left of the walker's (dbi block rows, dbs stripes), the path's likeliest
         // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
-        // diagonal, dbi + dbs*TD + |dbi - dbs*TD|.  Only the first nwin are recomputed ahead (the walker's
-        // own 2 x 2 tiles always rank first); speculative blocks cost the workers' time and the claims.
-        // Candidates up to 15 block rows / stripes away (4-bit offsets) in a cache 32 deep on both axes (the
-        // safety argument is at rc_block's cache store, ga_rcwalk.hip).  Deeper candidates keep the recompute
-        // ahead of a fast walker (C4, TD 4: a 28 us block against 27 us of walking across 8 block rows; round 3
-        // first searched 8 x 8).
-        const int span = c->knob("GA_RC_SPAN") ? std::max(2, std::min(ga::RC_SPAN_MAX, atoi(c->knob("GA_RC_SPAN"))))
-                                               : ga::RC_SPAN_MAX;
+        // diagonal, dbi + dbs*TD + cone*|dbi - dbs*TD| (cone 1 by default; GA_RC_CONE weighs the off-diagonal
+        // distance more, which reaches further along the diagonal with the same 64 blocks).  Only the first
+        // nwin are recomputed ahead (the walker's own 2 x 2 tiles always rank first); speculative blocks cost
+        // the workers' time and the claims.  Candidates up to 31 block rows / 7 stripes away (offsets dbi*8 + dbs)
+        // in a cache 64 x 32 deep (the safety argument is at rc_block's cache store, ga_rcwalk.hip).  Deeper
+        // candidates keep the recompute ahead of a fast walker (C4, TD 4: a 28 us block against 27 us of walking
+        // across 8 block rows; round 3 first searched 8 x 8, round 4 16 x 16: the default window is the same 64
+        // blocks in all three).
+        const int span = c->knob("GA_RC_SPAN") ? std::max(2, std::min(ga::RC_SPAN_I, atoi(c->knob("GA_RC_SPAN"))))
+                                               : ga::RC_SPAN_I;
+        const int cone = c->knob("GA_RC_CONE") ? std::max(1, std::min(8, atoi(c->knob("GA_RC_CONE")))) : 1;
         std::vector<std::pair<int, int>> off;
         for (int di = 0; di < span; di++)
-            for (int dj = 0; dj < span; dj++) off.push_back({di * 16 + dj, di + dj * TD + std::abs(di - dj * TD)});
+            for (int dj = 0; dj < std::min(span, ga::RC_SPAN_S); dj++)
+                off.push_back({di * 8 + dj, di + dj * TD + cone * std::abs(di - dj * TD)});
         // Liveness whatever the window's width: the walker waits only on tiles of its block and of the blocks
         // above it, left of it and up-left (its verified 2 x 2 tiles), so those four rank first (key -1);
         // ranked by the key alone, a 4-block window at TD = 4 held the walker's own stripe only, and one worker
         // never recomputed the stripe to its left (test_rc_worker_pools_vs_oracle[env0] timed out, round 4)
         for (auto& o : off)
-            if (o.first == 0 || o.first == 1 || o.first == 16 || o.first == 17) o.second = -1;
+            if (o.first == 0 || o.first == 1 || o.first == 8 || o.first == 9) o.second = -1;
         std::stable_sort(off.begin(), off.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
             return x.second < y.second;
         });
-        for (int k = 0; k < 64; k++) r.off[k] = (unsigned char)off[k].first;
-        // 64 of the 16 x 16 candidates (C3 walk 5.63 ms against 5.80 with 48 of 8 x 8, C4 with traceback 61 ms
-        // against 90: tools/exp/r3b_span.sh)
-        r.nwin = 64;
-        if (const char* e = c->knob("GA_RC_WIN")) r.nwin = std::max(4, std::min(64, atoi(e)));
+        for (int k = 0; k < 64; k++) r.off[k] = k < (int)off.size() ? (unsigned char)off[k].first : 0;
+        // 64 candidates (C3 walk 5.63 ms against 5.80 with 48 of 8 x 8, C4 with traceback 61 ms against 90:
+        // tools/exp/r3b_span.sh)
+        r.nwin = std::min(64, (int)off.size());
+        if (const char* e = c->knob("GA_RC_WIN")) r.nwin = std::max(4, std::min(r.nwin, atoi(e)));
     }
     // recompute workgroups: with a faster walker (scalar entry loads) fewer workers keep up, and more of them
     // slow the walker's own tile loads (C3 walk 5.78 / 5.84 / 5.99 / 6.24 ms at 48 / 64 / 96 / 128 workers,

@@ -328,19 +328,34 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
 
     if (reason < 0) {
         // ---- trip loop ----
+        // Tiles: the walker verifies the 2 x 2 tiles at its cell's tile (publishing that tile first: the loaders
+        // never evict a tile of the 4 x 4 block at the published tile; publish / tag read against the loaders'
+        // invalidate / re-check is ga_walk.h's Dekker handshake).  Every trip from a cell >= 10 rows and columns
+        // inside the verified region reads and lands inside it, so the walker re-verifies only when it comes within
+        // 10 of the region's top or left edge (about once per tile crossed).  One verification is one LDS round
+        // trip: lanes 0..3 read the four tags at once (4 dependent reads before: ~0.9 ms of C3's walk); only a
+        // missing tile is waited for.  (Verifying the 3 x 3 tiles ahead without blocking, round 5, blocked the walker
+        // on tiles two away that the loaders had not reached: slower.)
         int vlo_i = 1 << 30, vlo_j = 1 << 30;
-        // the tile of (pi, pj) and its neighbours above / to the left: every trip from a cell >= 10 rows and
-        // columns inside them reads and lands inside them
+        const unsigned tagbase = lds_addr(jtag);
         auto verify = [&](int pi, int pj) {
             const int thi = (pi - 1) >> 5, thj = (pj - 1) >> 5;
             const int tli = max(thi - 1, 0), tlj = max(thj - 1, 0);
-            const bool moved = thi != cti || thj != ctj;
-            if (moved) ntiles++;
-            need_tile(thi, thj, moved);
-            if (tlj != thj) need_tile(thi, tlj, false);
-            if (tli != thi) {
-                need_tile(tli, thj, false);
-                if (tlj != thj) need_tile(tli, tlj, false);
+            if (thi != cti || thj != ctj) {
+                ntiles++;
+                if (lane == 0) __hip_atomic_store(&jcur_tile, (thi << 16) | thj, __ATOMIC_SEQ_CST, WGS);
+            }
+            const int xi = (lane & 2) ? tli : thi, xj = (lane & 1) ? tlj : thj;
+            unsigned tv;
+            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(tv)
+                         : "v"(tagbase + 4u * (unsigned)jslot_of(xi, xj)) : "memory");
+            if (__builtin_amdgcn_ballot_w64(lane < 4 && tv != (unsigned)((xi << 16) | xj))) {
+                need_tile(thi, thj, false);
+                if (tlj != thj) need_tile(thi, tlj, false);
+                if (tli != thi) {
+                    need_tile(tli, thj, false);
+                    if (tlj != thj) need_tile(tli, tlj, false);
+                }
             }
             cti = thi;
             ctj = thj;
@@ -353,26 +368,31 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
         const unsigned dcol = (lane == 3 || lane == 4) ? 2u : 0u;
         const unsigned plane = 2u * JPLANE * (unsigned)(lane < 3 ? lane : lane < 6 ? lane - 3 : 0);
         const unsigned ebase = lds_addr(E) + plane;
-        const unsigned tbase = lds_addr(jrngbuf);
-        // One trip: t's entries and its successors' (lanes 0..5) and the table entry of dispatch D, one LDS round
-        // trip.  The loop is software-pipelined so that only the chain sits between a fetch landing and the next
-        // fetch going out: the entry taken (readlane), the advance (i, j: a mask and a bit count each), the next
-        // fetch's addresses; the level record (put), the move count and the region check run while it is in flight.
-        // A fetch whose cell has left the verified tiles reads harmless torus cells (the addresses are masked): the
-        // check after it then re-verifies and fetches again.
+        // the table: lanes 8..17 read dispatches d .. d+9 (a trip moves <= 9), so the next state's entry (dispatch
+        // d + k) is already in a register when its trip begins: lane 8 + k.  (The ring holds 4 blocks of 512
+        // dispatches; d+9 past a block boundary may read an older block: such an entry is only used after
+        // rng_ready, below.)
+        const unsigned tbase = lds_addr(jrngbuf) + 4u * (unsigned)(lane >= 8 && lane < 18 ? lane - 8 : 0);
+        // One trip: t's entries and its successors' (lanes 0..5), one LDS round trip.  The loop is software-
+        // pipelined so that only the chain sits between a fetch landing and the next fetch going out: the entry
+        // taken (readlane), the advance (i, j: a mask and a bit count each), the next fetch's addresses; the table
+        // read, the level record (put), the move count and the region check run while it is in flight.  A fetch
+        // whose cell has left the verified tiles reads harmless torus cells (the addresses are masked): the check
+        // after it then re-verifies and fetches again.
         auto fetch_e = [&](unsigned& v) {  // the entries: needs only (i, j)
             const unsigned roff = ((unsigned)(i - 1) & (JP - 1)) << 8, coff = ((unsigned)(j - 1) & (JP - 1)) << 1;
             const unsigned addr = ebase + (((roff - drow) & (2u * JP * (JP - 1))) | ((coff - dcol) & (2u * (JP - 1))));
             asm volatile("ds_read_u16 %0, %1" : "=v"(v) : "v"(addr));
             __builtin_amdgcn_sched_barrier(0);
         };
-        auto fetch_t = [&](unsigned& tb, int d) {  // the table entry of dispatch d
-            asm volatile("ds_read_b32 %0, %1" : "=v"(tb) : "v"(tbase + (((unsigned)d & (RB - 1)) << 2)));
+        auto fetch_t = [&](unsigned& tb, int d) {  // the table entries of dispatches d .. d+9
+            asm volatile("ds_read_b32 %0, %1" : "=v"(tb) : "v"(tbase + (((unsigned)d << 2) & (4u * (RB - 1)))));
         };
         auto outside = [&]() { return ((i - 10 - vlo_i) | (j - 10 - vlo_j)) < 0; };
         verify(i, j);
         if (!outside()) {
             unsigned v, tb;
+            int kprev = 0;
             fetch_e(v);
             fetch_t(tb, D);
             for (;;) {
@@ -385,24 +405,24 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
                 } else {
                     nties++;
                     // a tie: the table picks the level x; W = the tie move, then x's successor's run (none if a tie)
-                    const unsigned t = (unsigned)__builtin_amdgcn_readfirstlane((int)tb);
+                    const unsigned t = (unsigned)__builtin_amdgcn_readlane((int)tb, 8 + kprev);
                     const unsigned x = (t >> (((e >> 2) & 31u) + 3u)) & 3u;
                     const unsigned sx = (unsigned)__builtin_amdgcn_readlane((int)v, (int)(3u + x));
                     W = (((sx & 3u) ? sx : 0u) << 2) | jcode(x);
                 }
-                // the table entry first, then the entries (they land in issue order: the wait at the top of the
-                // loop is then the entries' own)
-                const int k = __builtin_popcount((W | (W >> 1)) & 0x55555u);
-                fetch_t(tb, D + k);
                 i -= __builtin_popcount(W & 0xaaaaau);
                 j -= __builtin_popcount(W & 0x55555u);
                 fetch_e(v);  // speculative while the region check below is pending
+                const int k = __builtin_popcount((W | (W >> 1)) & 0x55555u);
+                fetch_t(tb, D);
+                kprev = k;
                 if (__builtin_expect(((D + k) ^ D) >> 9, 0)) {
                     // a new block of table entries: the helper keeps the ring 3 blocks ahead, but make sure (and read
-                    // the entry again once it is there)
+                    // the entries again once they are there)
                     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v), "+v"(tb));
                     rng_ready(D + k);
                     fetch_t(tb, D + k);
+                    kprev = 0;
                 }
                 L = (int)jlevel((W >> (2 * k - 2)) & 3u);
                 // the moves as levels, MSB first: bit-reversing W swaps each field's two bits, and xor 3 maps the
@@ -416,6 +436,7 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
                     if (outside()) break;
                     fetch_e(v);
                     fetch_t(tb, D);
+                    kprev = 0;
                 }
             }
         }

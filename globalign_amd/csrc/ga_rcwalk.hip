@@ -12,8 +12,8 @@
 //                 stripe's 64*TD columns), stages the cells' traceback codes in LDS and writes the block's
 //                 words into the cache with write-through (sc1) stores, then the flag.
 // A block is 64 rows of one fill stripe: TD walker tiles.  The walk path only moves up and left, so the
-// window (up to 16 x 16 blocks up-left of the walker's block) always holds the tiles it can reach next, and a
-// 32 x 32-block cache never overwrites a block the walker may still read.  The words are the ones the
+// window (up to 32 block rows x 8 stripes up-left of the walker's block) always holds the tiles it can reach
+// next, and a 64 x 32-block cache never overwrites a block the walker may still read.  The words are the ones the
 // full traceback fill writes (lk_code of the same exact int32 cells), so the walk is unchanged.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -41,6 +41,37 @@ __device__ __forceinline__ void st16_sc1(uint4* p, uint4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
 }
 
+// A block's code window (dword i: a[base+i .. base+i+3]) and left-edge window (rows t0+1 ..) into LDS: four rounds of
+// loads issued before any store, so the block waits for one memory latency, not one per 64 entries.
+__device__ __forceinline__ void rc_windows(const RcArgs& r, uint32_t* awin, int2* ewin, int nst, int base, int t0, int s,
+                                           int lane) {
+    const int m = r.m;
+    for (int i0 = lane; i0 < nst + 72; i0 += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            v[q] = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int x = base + i0 + 64 * q + u;
+                v[q] |= (x >= 0 && x < m) ? (uint32_t)r.a[x] << (8 * u) : 0u;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i0 + 64 * q < nst + 72) awin[i0 + 64 * q] = v[q];
+    }
+    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
+    for (int i0 = lane; i0 < nst + 8; i0 += 256) {
+        int2 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = E[min(t0 + 1 + i0 + 64 * q, m)];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i0 + 64 * q < nst + 8) ewin[i0 + 64 * q] = v[q];
+    }
+}
+
 // Recompute block (bi, bs): rows 64*bi+1 .. 64*bi+64 of fill stripe bs, its traceback words into the cache.
 template <int TD, int CB>
 __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int bi, int bs, int lane) {
@@ -57,17 +88,8 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     const int base = t0 - 63;                               // a index of lane 63's row at step t0
     const int s = bs;
     const int j0 = s * 64 * TD, jl = j0 + lane * TD;
-    for (int i = lane; i < nst + 72; i += 64) {  // (a lane reads dwords up to nst + 67: one group ahead)
-        uint32_t v = 0;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int x = base + i + u;
-            v |= (x >= 0 && x < m) ? (uint32_t)r.a[x] << (8 * u) : 0u;
-        }
-        awin[i] = v;
-    }
-    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
-    for (int i = lane; i < nst + 8; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
+    // (a lane reads dwords up to nst + 67: one group ahead)
+    rc_windows(r, awin, ewin, nst, base, t0, s, lane);
     int bcode[TD];
     int H[TD], Y[TD];
     int Xl = 0, HLp = 0;
@@ -160,9 +182,9 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     // stripe of the cache (RC_CACHE_I * 4 * CB).  Only a block the walker can still reach is written: the walk
     // moves up and left and its loaders read tiles of the 4 x 4 block at its tile, so a block below the
     // walker's tile row, or right of its tile column, is never read again.  Safety: a block Y written now passed
-    // this check, so at this moment the walker's block row V is >= Y.  A block X sharing Y's slot (X = Y - 32k
-    // above it; the column axis is the same) is claimed only from a view V' of the walker with X >= V' - 15,
-    // i.e. V' <= Y - 17: after the walker has moved >= 17 block rows (>= 1088 steps, tens of us) past where it
+    // this check, so at this moment the walker's block row V is >= Y.  A block X sharing Y's slot (X = Y - 64k
+    // above it; the column axis alike with 32 and 7) is claimed only from a view V' of the walker with
+    // X >= V' - 31, i.e. V' <= Y - 33: after the walker has moved >= 33 block rows (>= 2112 steps) past where it
     // is now.  Y's stores issued here drain (vmcnt(0), rc_server) long before, so X's words, written after X's
     // recompute, are the slot's last.  (With a 16-deep cache and 16-deep candidates the margin was zero, and
     // two workers with different views could leave the walker another block's words)
@@ -218,17 +240,8 @@ __device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4*
     const int base = t0 - 63;
     const int s = bs;
     const int j0 = s * 64 * TD, jl = j0 + lane * TD;
-    for (int i = lane; i < nst + 72; i += 64) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int x = base + i + u;
-            v |= (x >= 0 && x < m) ? (uint32_t)r.a[x] << (8 * u) : 0u;
-        }
-        awin[i] = v;
-    }
-    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
-    for (int i = lane; i < nst + 8; i += 64) ewin[i] = E[min(t0 + 1 + i, m)];
+    // (a lane reads dwords up to nst + 67: one group ahead)
+    rc_windows(r, awin, ewin, nst, base, t0, s, lane);
     int bcode[TD];
     int H[TD], Y[TD];
     int Xl = 0, HLp = 0;
@@ -276,54 +289,72 @@ __device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4*
         eh[0] = e01.x; eh[1] = e01.z; eh[2] = e23.x; eh[3] = e23.z;
         ex[0] = e01.y; ex[1] = e01.w; ex[2] = e23.y; ex[3] = e23.w;
     };
+    // A group of 4 steps in two phases: the scores and every cell's LUT index first (a VALU chain), then the 4*TD
+    // LUT loads all in flight at once, then the entries (the E chains need the selectors).  Interleaved, the
+    // compiler kept two loads in flight and the block's steps waited on the LUT (44 us per C3 block).
     auto group = [&](int g, const int (&sb)[4][TD], const int (&eh)[4], const int (&ex)[4], auto MK) {
         constexpr bool MASKED = decltype(MK)::value;
+        unsigned idx[4][TD];
+        bool actv[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int row = t0 + g + u - lane + 1;
             const bool act = !MASKED || row >= 1;
+            actv[u] = act;
             int X = __builtin_amdgcn_update_dpp(ex[u], Xl, 0x138, 0xf, 0xf, false);
             const int HLn = __builtin_amdgcn_update_dpp(eh[u], Hl, 0x138, 0xf, 0xf, false);
-            // the left lane's last-column entries: E1 of this row (its step t-1), E0 of the row above (t-2)
-            int El = __builtin_amdgcn_update_dpp(0, E1last, 0x138, 0xf, 0xf, false);
-            int Ed = E0dgn;
-            E0dgn = __builtin_amdgcn_update_dpp(0, E0last, 0x138, 0xf, 0xf, false);
             int Hd = HLp;
-            // the block's rows go to the stage, the others to its scratch row
-            const unsigned rel = (unsigned)(row - R0 - 1);
-            uint16_t* dst = stage + (rel < 64u ? rel : 64u) * SC + lane * TD;
-            unsigned S01[TD], S2[TD];
 #pragma unroll
             for (int c = 0; c < TD; c++) {
                 const int sw = sb[u][c];
                 const int M = Hd + (int)(int8_t)(sw & 0xff);
                 const int Hn = min(min(M, X), Y[c]);
-                unsigned idx = min((unsigned)(X - Hn), op1) | (min((unsigned)(Y[c] - Hn), op1) << 4) |
-                               (min((unsigned)(M - Hn), 1u) << 8);
-                idx |= (unsigned)sw & 0x200u;  // a_i != b_j (bit 9 of the sub' table entry)
-                const uint4 f = lut[idx];
-                const unsigned Pd = ((unsigned)Ed << 2) | 3u, Pl = ((unsigned)El << 2) | 1u,
-                               Pu = ((unsigned)E2p[c] << 2) | 2u;
-                const unsigned src0 = __builtin_amdgcn_perm(Pl, Pd, 0x05040100u);
-                const unsigned E01 = __builtin_amdgcn_perm(src0, Pu, f.x);
-                const unsigned E2v = __builtin_amdgcn_perm(src0, Pu, f.y);
-                S01[c] = E01 | f.z;
-                S2[c] = E2v | f.w;
-                Ed = E0p[c];
-                El = (int)(E01 >> 16);
-                E0p[c] = act ? (int)(E01 & 0xffffu) : E0p[c];
-                E2p[c] = act ? (int)E2v : E2p[c];
+                idx[u][c] = min((unsigned)(X - Hn), op1) | (min((unsigned)(Y[c] - Hn), op1) << 4) |
+                            (min((unsigned)(M - Hn), 1u) << 8) | ((unsigned)sw & 0x200u);  // bit 9: a_i != b_j
                 const int Ho = Hn + o;
                 X = min(X, Ho);
                 Y[c] = act ? min(Y[c], Ho) : Y[c];
                 Hd = H[c];
                 H[c] = act ? Hn : H[c];
             }
-            E1last = act ? El : 0;
-            E0last = E0p[TD - 1];
             Xl = X;
             Hl = H[TD - 1];
             HLp = HLn;
+        }
+        uint4 f[4][TD];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int c = 0; c < TD; c++) f[u][c] = lut[idx[u][c]];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int row = t0 + g + u - lane + 1;
+            const bool act = actv[u];
+            // the left lane's last-column entries: E1 of this row (its step t-1), E0 of the row above (t-2)
+            int El = __builtin_amdgcn_update_dpp(0, E1last, 0x138, 0xf, 0xf, false);
+            int Ed = E0dgn;
+            E0dgn = __builtin_amdgcn_update_dpp(0, E0last, 0x138, 0xf, 0xf, false);
+            // the block's rows go to the stage, the others to its scratch row
+            const unsigned rel = (unsigned)(row - R0 - 1);
+            uint16_t* dst = stage + (rel < 64u ? rel : 64u) * SC + lane * TD;
+            unsigned S01[TD], S2[TD];
+#pragma unroll
+            for (int c = 0; c < TD; c++) {
+                const uint4 fc = f[u][c];
+                const unsigned Pd = ((unsigned)Ed << 2) | 3u, Pl = ((unsigned)El << 2) | 1u,
+                               Pu = ((unsigned)E2p[c] << 2) | 2u;
+                const unsigned src0 = __builtin_amdgcn_perm(Pl, Pd, 0x05040100u);
+                const unsigned E01 = __builtin_amdgcn_perm(src0, Pu, fc.x);
+                const unsigned E2v = __builtin_amdgcn_perm(src0, Pu, fc.y);
+                S01[c] = E01 | fc.z;
+                S2[c] = E2v | fc.w;
+                Ed = E0p[c];
+                El = (int)(E01 >> 16);
+                E0p[c] = act ? (int)(E01 & 0xffffu) : E0p[c];
+                E2p[c] = act ? (int)E2v : E2p[c];
+            }
+            E1last = act ? El : 0;
+            E0last = E0p[TD - 1];
             // the three levels' stored entries of this row's TD columns
             if constexpr (TD == 4) {
                 typedef unsigned u2v __attribute__((ext_vector_type(2)));
@@ -398,7 +429,7 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     if (wave >= r.workers) return;
     uint8_t* wl = dyn + (JUMP ? JWORK_OFF : 1024) + wave * r.worker_bytes;
     const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
-    const int dbi = r.off[lane] >> 4, dbs = r.off[lane] & 15;
+    const int dbi = r.off[lane] >> 3, dbs = r.off[lane] & 7;
     unsigned idle = 0;
     for (;;) {
         if (sgpr((int)g_ld(r.pos + 1))) break;  // the walk has ended

@@ -1,7 +1,7 @@
 """Round 5: the recompute walk's accounting at C3 (walker tile waits, tile loads, blocks recomputed and their time)
-per GA_RC_SERVERS:GA_RC_WIN config, one context per config (knobs are read when a context is created).
+per GA_RC_SERVERS:GA_RC_WIN[:GA_RC_CONE] config, one context per config (knobs are read when a context is created).
 
-    python tools/exp/r5/rc_diag.py [m] [servers:win ...]"""
+    python tools/exp/r5/rc_diag.py [m] [servers:win[:cone] ...]"""
 import ctypes as C
 import os
 import sys
@@ -25,9 +25,10 @@ mt0 = np.random.RandomState(0).randint(0, 2**32, size=625, dtype=np.uint64).asty
 mt0[624] = 624
 os.environ["GA_RC"] = "1"
 for cfg in cfgs:
-    ns, win = cfg.split(":")
+    ns, win, *rest = cfg.split(":")
     os.environ["GA_RC_SERVERS"] = ns
     os.environ["GA_RC_WIN"] = win
+    os.environ["GA_RC_CONE"] = rest[0] if rest else "1"
     eng = _native.Engine(0)
     eng.load(tables.codes(s1), tables.codes(s2), tables)
     for rep in range(2):
@@ -40,7 +41,7 @@ for cfg in cfgs:
         steps = len(r[1][0])
         jd = np.zeros(3, dtype=np.int32)
         L.ga_debug_walk_jump(eng._h, jd.ctypes.data)
-        print(f"steps={steps} ns_per_step={t['walk_ms'] * 1e6 / steps:.1f} servers={ns} win={win} fill={t['fill_ms']:.3f} "
+        print(f"steps={steps} ns_per_step={t['walk_ms'] * 1e6 / steps:.1f} servers={ns} win={win} cone={os.environ['GA_RC_CONE']} fill={t['fill_ms']:.3f} "
               f"walk={t['walk_ms']:.3f} call={t['call_ms']:.3f} kind={eng.fill_kind()} waits={w[0]} tiles={w[1]} "
               f"t_tile_ms={w[2] / 1e5:.3f} t_total_ms={w[4] / 1e5:.3f} loads={w[7]} load_us_avg={w[6] / max(w[7], 1) / 100:.2f} "
               f"| rc blocks={rc[2]} block_us_avg={rc[3] / max(rc[2], 1) / 100:.2f} | jump trips={jd[0]} rechecks={jd[1]} ties={jd[2]} "
