@@ -421,6 +421,12 @@ struct ga_ctx {
     uint32_t* rc_ops_pin = nullptr;
     int64_t rc_ops_cap = 0;  // words
     unsigned* rc_ops_prog = nullptr;
+    // rc_align's tie-break table: pinned staging, uploaded on a stream of its own while the fill runs, so that the walk
+    // is queued behind the fill at once (a pageable copy on the fill's stream held the calling thread to the fill's end)
+    uint32_t* up_pin = nullptr;
+    int64_t up_cap = 0;  // entries
+    hipStream_t ustream = nullptr;
+    hipEvent_t ev_up = nullptr;
     int rc_T = 0;          // its fill stripe width (64-column tiles per block)
     bool rc_jump = false;  // the last recompute walk was the tie-to-tie walk (jump entries)
     int rc_every_used = 64;
@@ -1585,7 +1591,24 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     c->rng_ms = (float)(now_ms() - t1);
     WalkBufs wb = ctx_walk_bufs(c);
     const int64_t ntab = (int64_t)R.tab.size();
-    HIPCHK(hipMemcpyAsync(wb.rng, R.tab.data(), sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, wb.stream));
+    // the table goes up on a stream of its own while the fill still runs (pinned staging: the copy is asynchronous),
+    // and the walk's stream waits for it: the walk launch below is then queued behind the fill at once
+    if (c->up_cap < ntab) {
+        if (c->up_pin) HIPCHK(hipHostFree(c->up_pin));
+        c->up_pin = nullptr;
+        c->up_cap = 0;
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, sizeof(uint32_t) * ntab, hipHostMallocDefault));
+        c->up_pin = static_cast<uint32_t*>(hp);
+        c->up_cap = ntab;
+    }
+    if (!c->ustream) HIPCHK(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, c->priority));
+    if (!c->ev_up) HIPCHK(hipEventCreateWithFlags(&c->ev_up, hipEventDisableTiming));
+    // (the last call's copy out of the staging buffer has ended: its walk waited for it, and the call for its walk)
+    std::memcpy(c->up_pin, R.tab.data(), sizeof(uint32_t) * ntab);
+    HIPCHK(hipMemcpyAsync(wb.rng, c->up_pin, sizeof(uint32_t) * ntab, hipMemcpyHostToDevice, c->ustream));
+    HIPCHK(hipEventRecord(c->ev_up, c->ustream));
+    HIPCHK(hipStreamWaitEvent(wb.stream, c->ev_up, 0));
     // the walk's levels go to pinned host memory, and this thread decodes them while the walk runs
     if (int r = pinned_walk_levels(c, wb)) return r;
     const WalkStart st0{m, n, 0, 0, 0, 1};
@@ -2313,6 +2336,9 @@ void ga_ctx_destroy(ga_ctx* c) {
     if (c->peer_link) (void)hipIpcCloseMemHandle(c->peer_link);
     if (c->rc_ops_pin) (void)hipHostFree(c->rc_ops_pin);
     if (c->rc_ops_prog) (void)hipHostFree(c->rc_ops_prog);
+    if (c->up_pin) (void)hipHostFree(c->up_pin);
+    if (c->ev_up) (void)hipEventDestroy(c->ev_up);
+    if (c->ustream) (void)hipStreamDestroy(c->ustream);
     for (auto& sl : c->pipe) {
         for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result, &sl.GVp, &sl.GHp,
                           &sl.top, &sl.left, &sl.bnd_row, &sl.bnd_col, &sl.meta, &sl.bscr})

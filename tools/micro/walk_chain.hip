@@ -63,6 +63,16 @@ __global__ void chain(long long* out, int* sink, int n) {
             L8 = (f >> 3) & 0x18u;
             acc += L8;
             t = t * 3u + 1u;
+        } else if (V == 7) {  // round 5: 64-bit table of lane deltas (up 8, left 17, diag 25) whose low 5 bits are
+            // also the next cell's field offset: readlane -> field offset -> table -> index (3 SALU), the level
+            // packed off the chain (bfe + lshl2_add)
+            const unsigned v = (unsigned)__builtin_amdgcn_readlane(win, (int)idx);
+            const unsigned s = v >> L8;
+            const unsigned long long t64 = ((unsigned long long)t << 32) | t;
+            const unsigned Vx = (unsigned)(t64 >> (s & 63u));
+            idx += Vx;
+            L8 = Vx;
+            acc = acc * 4u + __builtin_amdgcn_ubfe(Vx, 3u, 2u);
         } else if (V == 2) {  // eight dependent scalar ops (no readlane)
             idx = ((idx >> 3) ^ t) + 1u;
             idx = (idx >> (idx & 7u)) & 0xffffu;
@@ -95,6 +105,7 @@ int main() {
     printf("readlane -> s_add -> readlane : %.1f cyc\n", run(chain<1>));
     printf("walker step, 64-bit table     : %.1f cyc\n", run(chain<3>));
     printf("8 dependent SALU ops          : %.1f cyc\n", run(chain<2>));
+    printf("lane-delta table (3 SALU)     : %.1f cyc\n", run(chain<7>));
     printf("walker step, SGPR window      : %.1f cyc\n", run(chain<4>));
     printf("next-state words (1 SALU)     : %.1f cyc\n", run(chain<5>));
     printf("next-state words + 8 VALU     : %.1f cyc\n", run(chain<6>));
