@@ -60,6 +60,10 @@ struct FillArgs {
     int out_wave;             // lane fill (NWC <= 4): the out-path in a wave of its own (GA_LANE_OUTWAVE; 0: the IO wave's)
     int hand_scope;           // lane fill: workgroup hand-off polls with system-scope loads (1), and stores (2)
     int xcd_map;              // lane fill, one round of workgroups: chain neighbours on one XCD (ga_lane.hip lane_slab)
+    // lane fill: the query profile of this fill's rows in HBM (launch_lane_qprof, [K][m + 4] dwords, dword r + 2 = the
+    // sub' bytes of rows r .. r+3 of one column code, rows outside 1..m zero), copied into the LDS ring by the profile
+    // wave; nullptr: the profile wave computes it from a and sub'
+    const uint32_t* qprof;
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),
@@ -176,5 +180,7 @@ size_t fill_diag_lds_bytes(int nwc, int qbytes, int K, int qrows);
 // traceback words (p.tb != nullptr, CB bytes per cell), int8 profile, K <= 32, qrows = profile rows, a power of two)
 void launch_fill_lane(hipStream_t s, const FillArgs& p, int CB);
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows);
+// the lane fill's query profile (FillArgs::qprof) of rows a[0 .. m-1]: K x (m + 4) dwords at out
+void launch_lane_qprof(hipStream_t s, const uint8_t* a, int m, const int* subp, int K, uint32_t* out);
 
 }  // namespace ga

@@ -406,6 +406,7 @@ struct ga_ctx {
     DevBuf dbg, wdbg;
     // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
     DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
+    DevBuf qprof;  // the lane fill's query profile (ga::launch_lane_qprof), rebuilt by every lane fill
     int walk_jump_diag[3] = {0, 0, 0};  // the tie-to-tie walk's trips, region re-checks, ties (result[12..14])
     DevBuf jlut;           // the jump workers' LUT for gap open jlut_o (ga::jump_lut_build)
     int jlut_o = -1;
@@ -925,6 +926,14 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     if (c->dbg_on) HIPCHK(c->dbg.ensure(sizeof(unsigned long long) * ga::LK_DBG_WORDS * c->nstripes));
     if (c->dbg_on) HIPCHK(hipMemsetAsync(c->dbg.p, 0, sizeof(unsigned long long) * ga::LK_DBG_WORDS * c->nstripes, st));
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
+    // the lane fill's query profile, built on the fill's stream just before it (K x (m + 4) dwords: C5 1.9 MB, a few us).
+    // Fills of one problem in flight on other streams (align_many) rewrite it with the same values.
+    p.qprof = nullptr;
+    if (c->lane && !c->xknob("GA_LANE_QPROF_WAVE")) {  // (experiments build: the profile wave builds it, for A/B)
+        HIPCHK(c->qprof.ensure(sizeof(uint32_t) * (size_t)c->K * (size_t)(m + 4)));
+        ga::launch_lane_qprof(st, p.a, (int)m, p.subp, c->K, c->qprof.as<uint32_t>());
+        p.qprof = c->qprof.as<uint32_t>();
+    }
     HIPCHK(hipEventRecord(bd.ev0 ? bd.ev0 : c->ev[0], st));
     if (c->lane) ga::launch_fill_lane(st, p, c->CB);
     else if (c->diag) ga::launch_fill_diag(st, p, c->qbytes, full);
@@ -2330,7 +2339,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
                       &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt, &c->colck, &c->stck,
-                      &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->link})
+                      &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->link, &c->qprof})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     if (c->peer_link) (void)hipIpcCloseMemHandle(c->peer_link);

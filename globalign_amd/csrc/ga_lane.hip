@@ -77,6 +77,30 @@ __device__ unsigned lane_slab(const FillArgs& p) {
     return start + rk;
 }
 
+// The query profile of a lane fill's rows (FillArgs::qprof): dword r + 2 of code c (r = -2 .. m + 1) holds sub'(a_r .. a_r+3, c)
+// as int8 bytes, rows outside 1..m zero -- the dwords the profile wave used to build per row from a and sub' (for a
+// 24-code alphabet 96 LDS byte reads and 24 writes per lane per 64 rows: at C5 it fell behind the chain's head, which
+// then waited on it for 32 % of its steps, round 5, profiles/r05/c5_stamps.txt); one thread per dword
+__global__ void __launch_bounds__(256) lane_qprof_kernel(const uint8_t* __restrict__ a, int m, const int* __restrict__ subp,
+                                                         int K, uint32_t* __restrict__ out) {
+    const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int pitch = m + 4;
+    if (q >= (long long)K * pitch) return;
+    const int c = (int)(q / pitch), r = (int)(q % pitch) - 2;
+    uint32_t v = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int row = r + u;
+        if (row >= 1 && row <= m) v |= (uint32_t)(uint8_t)(int8_t)subp[a[row - 1] * K + c] << (8 * u);
+    }
+    out[q] = v;
+}
+
+void launch_lane_qprof(hipStream_t s, const uint8_t* a, int m, const int* subp, int K, uint32_t* out) {
+    const long long nq = (long long)K * (m + 4);
+    lane_qprof_kernel<<<dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s>>>(a, m, subp, K, out);
+}
+
 size_t fill_lane_lds_bytes(int nwc, int K, int qrows) {
     return (size_t)LK_HEAD_BYTES + (size_t)(nwc + 1) * RING * sizeof(int2) + (size_t)K * (qrows + LK_QMIRROR) * 4 +
            (size_t)K * 32;  // + the K x K int8 sub' table (K <= 32)
@@ -310,7 +334,28 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                 if (slot < (unsigned)LK_QMIRROR) pq[c * QS + QR + slot] = v;
             }
         };
-        if (lane < 3) put_dword(lane - 2);
+        // the precomputed profile (p.qprof): K dword loads and LDS stores per lane per 64 rows, loads in flight together
+        const int qpitch = m + 4;
+        auto copy_dword = [&](int r) {
+            const unsigned slot = (unsigned)(r - 1) & qmask;
+            const uint32_t* src = p.qprof + (r + 2);
+            for (int c0 = 0; c0 < K; c0 += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = c0 + u < K ? src[(long long)(c0 + u) * qpitch] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    if (c0 + u < K) {
+                        pq[(c0 + u) * QS + slot] = v[u];
+                        if (slot < (unsigned)LK_QMIRROR) pq[(c0 + u) * QS + QR + slot] = v[u];
+                    }
+                }
+            }
+        };
+        if (lane < 3) {
+            if (p.qprof) copy_dword(lane - 2);
+            else put_dword(lane - 2);
+        }
         unsigned q_next = 0, spins = 0;
         while (q_next < (unsigned)m) {
             // the slowest wave reads rows above (its output rows) - 16, so slots of rows below that + QR are free
@@ -319,7 +364,10 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
             const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
             if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
                 const unsigned r = q_next + 1 + lane;
-                if (r <= hi) put_dword((int)r);
+                if (r <= hi) {
+                    if (p.qprof) copy_dword((int)r);
+                    else put_dword((int)r);
+                }
                 if (lane == 0) lds_st(&cnt[LK_PRODQ], hi == (unsigned)m ? LK_DONE : hi);
                 q_next = hi;
                 spins = 0;

@@ -15,8 +15,13 @@ from globalign_amd import _native  # noqa: E402
 
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 cfgs = sys.argv[2:] or ["64:64"]
-s1, s2 = bench.splitmix(m, 1), bench.splitmix(m, 2)
-tables, _ = bench.problem_tables(s1, s2)
+wl = bench.WORKLOADS.get(os.environ.get("RC_WL", ""))  # (RC_WL=c5: that workload's alphabet, seeds and scoring)
+if wl:
+    s1, s2 = bench.splitmix(m, wl["seeds"][0], wl["alphabet"]), bench.splitmix(m, wl["seeds"][1], wl["alphabet"])
+    tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
+else:
+    s1, s2 = bench.splitmix(m, 1), bench.splitmix(m, 2)
+    tables, _ = bench.problem_tables(s1, s2)
 L = _native.load_library()
 L.ga_debug_walk.argtypes = [C.c_void_p, C.c_void_p]
 L.ga_debug_rc.argtypes = [C.c_void_p, C.c_void_p]
