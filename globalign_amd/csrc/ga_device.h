@@ -19,6 +19,10 @@ constexpr int GOUT = GA_GOUT;    // rows per cross-workgroup publish (4: C3 cros
 constexpr int HAND_SENT = (int)0x80808080u;
 constexpr int FILL_LDS_MIN = 82 * 1024;  // > 80 KB: one fill workgroup per CU
 
+// the recompute fill's right-edge checkpoints: a stripe's rows 0..m, then this many scratch slots of its own (a store's
+// offset from the stripe's base then fits the 32-bit VGPR offset of a global store with an SGPR base)
+constexpr int COLCK_PAD = 64;
+
 struct FillArgs {
     const uint8_t* a;         // m codes (seq_1)
     const int* subp;          // K x K: sub'(x, y) = sub(x, y) - gV(x) - gH(y)
@@ -43,11 +47,13 @@ struct FillArgs {
     int2* ckpt;               // banded traceback: (H', h2') of rows ckpt_rows, 2*ckpt_rows, ... (< m) or nullptr
     int ckpt_rows;            //   [row / ckpt_rows - 1][n + 1]; a multiple of FROWS
     // recompute checkpoints of the lane fill (nullptr: none)
-    int2* colck;              // [nstripes][m + 1]: (H', h1') of every stripe's right edge column, rows 1..m; then 64
-                              // scratch slots (the lean sub-chunk's lanes that carry no row store there)
+    int2* colck;              // [nstripes][m + 1 + COLCK_PAD]: (H', h1') of every stripe's right edge column, rows
+                              // 1..m, then 64 scratch slots of the stripe (the lean sub-chunk's lanes that carry no
+                              // row store there)
     int2* stck;               // staircase lane states after step k*stck_every - 1, k = 1 .. (m - 1) / stck_every:
                               //   [k - 1][nstripes][TD + 1][64]: (H'[c], h2'[c]) for c < TD, then (h1' carry, H' diag)
-    int stck_every;           //   a multiple of 32 (a pair of 16-step sub-chunks)
+    int stck_every;           //   a power of two >= 64 (pairs of 16-step sub-chunks)
+    int stck_shift;           //   log2(stck_every)
     int late;                 // lane fill, score only: late edge reads (one-round chains; ga_lane.hip LATE)
     int hand_direct;          // lane fill: the last compute wave stores the hand-off rows (else the IO wave)
     // tuning overrides from the context's knobs (ga_ctx::knobs; < 0: the default): LDS floor per workgroup
@@ -121,7 +127,7 @@ struct RcArgs {
     int K;
     const int2* top;       // [n+1] (H', h2') of row 0
     const int2* left;      // [m+1] (H', h1') of column 0
-    const int2* colck;     // [nstripes][m+1] right edges (FillArgs::colck)
+    const int2* colck;     // [nstripes][m + 1 + COLCK_PAD] right edges (FillArgs::colck)
     const int2* stck;      // staircase states (FillArgs::stck)
     int stck_every;
     uint8_t* tb;           // traceback words (ga_device.h layout), TC 16-byte words per lane per 64-column stripe

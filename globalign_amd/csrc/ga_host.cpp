@@ -846,6 +846,8 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.hand_direct = 0;  // measured: C4 210 ms against 221 with the direct hand-off, 1M x 125k 52.5 against 56 (r3_c4.log)
     if (const char* e = c->knob("GA_LANE_DIRECT")) p.hand_direct = atoi(e);
     p.stck_every = every;
+    p.stck_shift = 0;
+    while ((1 << p.stck_shift) < every) p.stck_shift++;
     {
         const char* e = c->knob("GA_FILL_LDS_FLOOR");
         p.lds_floor = e ? atoi(e) : -1;
@@ -873,7 +875,7 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // fails the second allocation after the first succeeded.
         const bool fail_test = c->knob("GA_RC_FAIL_ALLOC") && atoi(c->knob("GA_RC_FAIL_ALLOC")) == 1;
         int nb = 0;
-        for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * ((size_t)c->nstripes * (m + 1) + 64)},
+        for (auto [buf, bytes] : {std::pair<DevBuf*, size_t>{&c->colck, sizeof(int2) * (size_t)c->nstripes * (m + 1 + ga::COLCK_PAD)},
                                   {&c->stck, sizeof(int2) * (size_t)nck * c->nstripes * (c->T + 1) * 64}}) {
             hipError_t e = buf->ensure(bytes);
             if (e == hipSuccess && fail_test && nb == 1) e = hipErrorOutOfMemory;
@@ -1297,10 +1299,13 @@ bool rc_eligible(ga_ctx* c) {
 
 // checkpoint spacing (steps; a multiple of 32): 64 keeps a block's recompute at <= 127 + 63 steps; wider
 // The checkpoint spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per
-// spacing: chosen with the geometry in enqueue_fill; GA_RC_EVERY (a multiple of 32, >= 64) fixes it
+// spacing: chosen with the geometry in enqueue_fill; GA_RC_EVERY (a power of two >= 64; rounded down) fixes it
 int rc_every_req(const ga_ctx* c) {
     const char* e = c->knob("GA_RC_EVERY");
-    return e ? std::max(64, (atoi(e) / 32) * 32) : 0;
+    if (!e) return 0;
+    int v = 64;
+    while (2 * v <= atoi(e) && v < (1 << 20)) v *= 2;
+    return v;
 }
 
 // The score-only checkpointing fill of the loaded problem or slab.

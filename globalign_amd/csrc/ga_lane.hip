@@ -441,8 +441,12 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     unsigned pc_lds = lds_addr(&cnt[2 * w]);  // {cons(w), prod(w + 1)}: one 8-byte store
     const unsigned rout_lds = lds_addr(rout);
     // the recompute checkpoints' right edge of this stripe, and a scratch slot per lane past all of them
-    int2* const colck_s = RC && p.colck != nullptr ? p.colck + (long long)s * (m + 1) : nullptr;
-    int2* const colck_x = RC && p.colck != nullptr ? p.colck + ((long long)p.nstripes * (m + 1) + lane) : nullptr;
+    int2* const colck_s = RC && p.colck != nullptr ? p.colck + (long long)s * (m + 1 + COLCK_PAD) : nullptr;
+    int2* const colck_x = RC && p.colck != nullptr ? colck_s + (m + 1 + lane) : nullptr;
+    // the lean steady state's checkpoint store: the stripe's base in SGPRs and a 32-bit offset per lane, rows
+    // rlo + lane - 48 (lanes 48..63; LEAN sub-chunks hold no row past m) or the lane's scratch slot: off = cb + cm * rlo
+    const unsigned ck_cb = lane >= 48 ? (unsigned)(lane - 48) * 8u : (unsigned)(m + 1 + lane) * 8u;
+    const unsigned ck_cm = lane >= 48 ? 8u : 0u;
     unsigned avail = 0, outfree = 0, qavail = 0;
     bool aborted = false;
     unsigned long long wcyc[3] = {0, 0, 0}, t_start = 0, c_start = 0;
@@ -498,16 +502,17 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     // the step of a sub-chunk at which score-only waves await and read the next sub-chunk's edges
     // (0: after the first step, as the traceback variants do)
     constexpr int LE = (CB == 0 && !CKP && SUB == 16 && LATE) ? GA_LANE_LE : 0;
-    // lanes 64-SUB .. 63: the shift registers' rows of a sub-chunk
-    unsigned long long out_mask = SUB == 16 ? 0xffff000000000000ull : 0xff00000000000000ull;
 
     // one SUB-step sub-chunk: steps r0 .. r0+SUB-1 from C / qc; after its first step the next
     // sub-chunk's edges, profile windows and the producer's counter are read into Nx / qx / pnext (they
     // land while the other steps run); then lanes 64-SUB..63 store lane 63's SUB rows and lane 0
     // publishes {cons(w) = r0 + 2 SUB, prod(w + 1)} in one 8-byte store
+    // LEAN (the steady state of the lean sub-chunk, see the main loop): the sub-chunk is known unmasked and lean, so no
+    // per-sub-chunk test of r0 / tm / the knobs sits between the statements
     auto sub_chunk = [&](int r0, int4 (&C)[NE], int4 (&Nx)[NE], uint32_t (&qc)[TD][NQ], uint32_t (&qx)[TD][NQ],
-                         auto HALF) {
+                         auto HALF, auto LEANT) {
         constexpr int HB = decltype(HALF)::value * SUB;  // the sub-chunk's first step in its 16-step window
+        constexpr bool LEAN = decltype(LEANT)::value;
         if (!LE) {
             avail = sgpr_u(max(avail, pnext));
             if ((int)avail < r0 + 2 * SUB) wait_ge(prod_in, 0, avail, r0 + 2 * SUB, 0);
@@ -602,9 +607,9 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                 steps(std::false_type{}, std::false_type{});
             }
         } else {
-            const bool masked = r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB;
+            const bool masked = !LEAN && (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB);
             if constexpr (ASMOK) {
-                if (use_asm && !masked && !hand_direct) {
+                if (LEAN || (use_asm && !masked && !hand_direct)) {
                     // The lean sub-chunk: the 16 steps, the next sub-chunk's profile and edge reads
                     // and lane 63's rows out as ONE asm statement (LaneSub, ga_lane_asm.h), so that no compiler code,
                     // copy or conservative wait sits between the steps.  Lane 63's rows go out by DPP moves into
@@ -660,7 +665,12 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                         qx[k][2] = qn[k][1].x;
                         qx[k][3] = qn[k][1].y;
                     }
-                    if (RC && p.colck != nullptr) {
+                    if (RC && LEAN) {
+                        // (colck is set whenever the RC variant runs, enqueue_fill) one offset and one store
+                        const lk_v2u vv = (lane & 4) ? lk_v2u{(unsigned)R[0], (unsigned)R[1]} : lk_v2u{(unsigned)R[2], (unsigned)R[3]};
+                        const unsigned off = ck_cb + ck_cm * (unsigned)rlo;
+                        asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(off), "v"(vv), "s"(colck_s) : "memory");
+                    } else if (RC && p.colck != nullptr) {
                         // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge; every lane stores (lanes
                         // without a row into the scratch slots past the checkpoints): no exec change, which would
                         // drain the VALU pipeline on every sub-chunk (the direct hand-off takes the compiler's steps)
@@ -675,9 +685,12 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                     return;
                 }
             }
-            if (masked) steps(std::true_type{}, std::false_type{});
-            else steps(std::false_type{}, std::false_type{});
+            if constexpr (!LEAN) {
+                if (masked) steps(std::true_type{}, std::false_type{});
+                else steps(std::false_type{}, std::false_type{});
+            }
         }
+        if constexpr (!LEAN) {
         // lane 63 computed rows r0-62 .. r0-63+SUB; lanes 64-SUB..63 of the shift registers hold them
         const int rlo = r0 - 62;
         if ((int)outfree < rlo + SUB - 1) wait_ge(cons_out, RING, outfree, rlo + SUB - 1, 2);
@@ -687,17 +700,19 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
         unsigned long long saved;
         const unsigned pcl = pc_lds;            // (a generic lambda's asm operands must be its own locals)
-        const unsigned long long om = out_mask;
+        // exec = lanes 64-SUB .. 63 as literals (an SGPR operand for the mask was given a VGPR pair in the TD 8 variant
+        // once the lean steady state doubled the loop body)
         asm volatile(
             "s_mov_b64 %0, exec\n\t"
-            "s_mov_b64 exec, %4\n\t"
+            "s_mov_b32 exec_lo, 0\n\t"
+            "s_mov_b32 exec_hi, %4\n\t"
             "ds_write_b64 %1, %2\n\t"
             "s_mov_b64 exec, 1\n\t"
             "ds_write_b64 %3, %5\n\t"
             "s_mov_b64 exec, %0\n\t"
             "s_nop 4"
             : "=&s"(saved)
-            : "v"(oaddr), "v"(hx), "v"(pcl), "s"(om), "v"(cp)
+            : "v"(oaddr), "v"(hx), "v"(pcl), "n"(SUB == 16 ? (int)0xffff0000u : (int)0xff000000u), "v"(cp)
             : "memory");
         if (hand_direct) {
             // the workgroup's right edge straight to its hand-off rows (agent-scope 8-byte stores, each row
@@ -712,8 +727,9 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
             // lane 64-SUB+u holds row rlo+u of this stripe's right edge
             const int row = rlo + lane - (64 - SUB);
             if (p.colck != nullptr && lane >= 64 - SUB && row >= 1 && row <= m)
-                p.colck[(long long)s * (m + 1) + row] = make_int2(RH, RX);
+                colck_s[row] = make_int2(RH, RX);
         }
+        }  // !LEAN
     };
     // traceback words: window w of 16 steps done -> aligned word w - 1 - lane/16 of every column (LkRot)
     auto emit = [&](int win) {
@@ -743,26 +759,86 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     // words a 16-step window is a pair of 8-step sub-chunks or one 16-step sub-chunk
     static_assert(CB == 0 || SUB == 8 || SUB == 16, "traceback windows are 16 steps");
     const int nit = (16 * nwin + 2 * SUB - 1) / (2 * SUB);
-    for (int it = 0; it < nit; it++) {
-        const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
-        if (CB > 0 && SUB == 16) {
-            sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
-            emit(2 * it);
-            sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 0>{});
-            emit(2 * it + 1);
-        } else {
-            sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{});
-            sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{});
-            emit(it);
+    // The lean sub-chunk's steady state: iterations [it_lo, it_hi) run it with no per-sub-chunk test (from row 64 on, every
+    // lane is inside the matrix; a partial stripe's last lane reaches row m at step tm, and the sub-chunks near it are
+    // masked); the iterations before and after take the tested path
+    // (not at TD 8: the second copy of the loop body pushed the C4 variant past 256 VGPRs into scratch, 6x slower)
+    constexpr bool LEANOK = ASMOK && TD <= 4;
+    int it_lo = nit, it_hi = nit;
+    if constexpr (LEANOK) {
+        if (use_asm && !hand_direct) {
+            it_lo = min(64 / (2 * SUB), nit);
+            // every sub-chunk x of [it_lo, it_hi) has x <= tm - SUB: (unsigned)(tm - x) >= SUB
+            it_hi = !partial ? nit : tm - 3 * SUB + 1 >= 0 ? min(nit, (tm - 3 * SUB + 1) / (2 * SUB) + 1) : 0;
+            // RC: and no row past m in a lean sub-chunk (its checkpoint store does not test): r0 + SUB - 62 + 15 <= m
+            if (RC) it_hi = min(it_hi, (m + 31) / (2 * SUB) + 1);
+            it_hi = max(it_hi, it_lo);
         }
-        if constexpr (RC) {
-            // staircase checkpoint k after step k*E - 1: lane 0 has finished row k*E, lane l row k*E - l
-            const int done = r0 + 2 * SUB;
-            if (p.stck_every > 0 && done % p.stck_every == 0 && done < m) {
-                int2* ck = p.stck + ((long long)(done / p.stck_every - 1) * p.nstripes + s) * (TD + 1) * 64 + lane;
+    }
+    if constexpr (LEANOK) {
+        // every global load of the prologue (p.top, p.b, ...) landed: said once here, with the intrinsic the compiler's
+        // wait insertion understands, since the path around an empty first loop otherwise left them "pending" into the
+        // lean loop, whose statements then each waited for every outstanding memory operation (s_waitcnt vmcnt(0))
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        auto iteration = [&](int it, auto LEANT) {
+            const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
+            if (CB > 0 && SUB == 16) {
+                sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, LEANT);
+                emit(2 * it);
+                sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 0>{}, LEANT);
+                emit(2 * it + 1);
+            } else {
+                sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, LEANT);
+                sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{}, LEANT);
+                emit(it);
+            }
+            if constexpr (RC) {
+                // staircase checkpoint k after step k*E - 1: lane 0 has finished row k*E, lane l row k*E - l
+                // (the spacing is a power of two: a mask and a shift, not a division per iteration).  The stores are
+                // asm with the checkpoint's base in SGPRs: as compiler stores they made it wait for every outstanding
+                // store (s_waitcnt vmcnt(0)) before the next lean statement, i.e. for the checkpoint stores' round trip
+                // to memory on every iteration (the recompute fill 0.7 ms slower than the plain one at C3)
+                const int done = r0 + 2 * SUB;
+                if (p.stck_every > 0 && (done & (p.stck_every - 1)) == 0 && done < m) {
+                    const int2* ck = p.stck + ((long long)((done >> p.stck_shift) - 1) * p.nstripes + s) * (TD + 1) * 64;
+                    const unsigned loff = (unsigned)lane * 8u;
 #pragma unroll
-                for (int k = 0; k < TD; k++) ck[k * 64] = make_int2(H[k], Y[k]);
-                ck[TD * 64] = make_int2(Xl, HLp);
+                    for (int k = 0; k <= TD; k++) {
+                        const lk_v2u vv = k < TD ? lk_v2u{(unsigned)H[k], (unsigned)Y[k]} : lk_v2u{(unsigned)Xl, (unsigned)HLp};
+                        asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(loff), "v"(vv), "s"(ck), "n"(k * 512)
+                                     : "memory");
+                    }
+                }
+            }
+        };
+        int it = 0;
+        for (; it < it_lo; it++) iteration(it, std::false_type{});
+        for (; it < it_hi; it++) iteration(it, std::true_type{});
+        for (; it < nit; it++) iteration(it, std::false_type{});
+    } else {
+        // the loop body written out (an extra lambda layer kept the traceback variants' sub-chunks out of line and
+        // their register arrays in scratch)
+        for (int it = 0; it < nit; it++) {
+            const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
+            if (CB > 0 && SUB == 16) {
+                sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, std::false_type{});
+                emit(2 * it);
+                sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 0>{}, std::false_type{});
+                emit(2 * it + 1);
+            } else {
+                sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, std::false_type{});
+                sub_chunk(r0 + SUB, B, A, qB, qA, std::integral_constant<int, 1>{}, std::false_type{});
+                emit(it);
+            }
+            if constexpr (RC) {
+                // staircase checkpoint k after step k*E - 1: lane 0 has finished row k*E, lane l row k*E - l
+                const int done = r0 + 2 * SUB;
+                if (p.stck_every > 0 && (done & (p.stck_every - 1)) == 0 && done < m) {
+                    int2* ck = p.stck + ((long long)((done >> p.stck_shift) - 1) * p.nstripes + s) * (TD + 1) * 64 + lane;
+#pragma unroll
+                    for (int k = 0; k < TD; k++) ck[k * 64] = make_int2(H[k], Y[k]);
+                    ck[TD * 64] = make_int2(Xl, HLp);
+                }
             }
         }
     }
@@ -784,6 +860,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     }
 }
 
+#ifndef GA_LANE_KERNEL_ONLY  // (a test unit compiles one kernel variant alone)
 template <int NWC, int TD, int CB, int SUB, bool DBG = false>
 static void launch_lane_one(hipStream_t s, const FillArgs& p) {
     // the recompute checkpoints exist in one variant only (no timestamps, 16-step sub-chunks): enqueue_fill
@@ -873,5 +950,6 @@ void launch_fill_lane(hipStream_t s, const FillArgs& p, int CB) {
     else if (CB == 2) launch_lane_cb<2>(s, p);
     else launch_lane_cb<4>(s, p);
 }
+#endif  // GA_LANE_KERNEL_ONLY
 
 }  // namespace ga

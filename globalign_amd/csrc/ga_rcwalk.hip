@@ -61,7 +61,7 @@ __device__ __forceinline__ void rc_windows(const RcArgs& r, uint32_t* awin, int2
         for (int q = 0; q < 4; q++)
             if (i0 + 64 * q < nst + 72) awin[i0 + 64 * q] = v[q];
     }
-    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1);
+    const int2* E = s == 0 ? r.left : r.colck + (long long)(s - 1) * (m + 1 + COLCK_PAD);
     for (int i0 = lane; i0 < nst + 8; i0 += 256) {
         int2 v[4];
 #pragma unroll
