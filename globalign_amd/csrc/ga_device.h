@@ -96,8 +96,9 @@ struct WalkArgs {
     int skip_corners;     // loaders leave the block's far off-diagonal tiles (offsets (3,0), (0,3), (3,1), (1,3))
     int nloaders;         // loader waves: 12, 13 (+ the idle wave 12) or 14 (+ wave 8, no L2 prefetcher)
     // the recompute walk (walk_rc_kernel; unused by the other walks)
-    const unsigned* rc_flags;  // [nbi][nbs] per 64-row block of a fill stripe: rc_ready once its words are written
+    unsigned* rc_flags;        // [nbi][nbs] per 64-row block of a fill stripe: rc_ready once its words are written
     unsigned rc_ready;
+    unsigned long long* rc_own;  // [RC_CACHE_I][RC_CACHE_S] the block whose words a cache slot holds (rc_slot_tag)
     int rc_nbs, rc_td;         // blocks per block row; 64-column tiles per block (the fill's TD)
     unsigned* rc_pos;          // [0] the walker's tile (ti << 16 | tj), [1] 1 once the walk has ended
     // optional (nullptr): dispatches whose levels are in `ops` (pinned host memory then), raised by the
@@ -118,6 +119,16 @@ constexpr int RC_SPAN_S = 8;
 constexpr int RC_CACHE_I = 2 * RC_SPAN_I;
 constexpr int RC_CACHE_S = 32;
 
+// A cache slot's owner tag: the block whose words the slot holds, with the call's ready value, or 0 while
+// a worker that claimed a block of that slot may be rewriting it.  The worker clears the tag before its first word
+// store and sets it after the last, then raises the block's flag; a loader reads the tag before and after it copies
+// a tile, so words another block's worker overwrote are never used, whatever the timing (the reach check's margin
+// alone made that a matter of timing), and a ready flag whose slot has lost its words is reset for a recompute.
+__host__ __device__ inline unsigned long long rc_slot_tag(int bi, int bs, int nbs, unsigned ready) {
+    return ((unsigned long long)((unsigned)bi * (unsigned)nbs + (unsigned)bs + 1u) << 32) | ready;
+}
+__host__ __device__ inline int rc_slot(int bi, int bs) { return (bi % RC_CACHE_I) * RC_CACHE_S + bs % RC_CACHE_S; }
+
 // The recompute workgroups of walk_rc_kernel (ga_rcwalk.hip): each wave recomputes 64-row
 // blocks of one fill stripe (64*TD columns) from the lane fill's checkpoints, writing their traceback words.
 struct RcArgs {
@@ -135,6 +146,8 @@ struct RcArgs {
     int TD, nstripes, nbi, nbs;  // nbs = nstripes; nbi = 64-row blocks
     unsigned* flags;       // [nbi][nbs]: < 2*epoch free, 2*epoch claimed, 2*epoch + 1 ready
     unsigned epoch;
+    unsigned long long* own;  // WalkArgs::rc_own
+    int tag_fault;            // test knob GA_RC_TAG_FAULT=k: each worker leaves the tag of every k-th block unset
     unsigned* pos;         // the walk's WalkArgs::rc_pos
     int tile0;             // the walk's first tile (ti << 16 | tj), until it publishes one
     int workers;           // waves per workgroup that recompute (the rest leave)

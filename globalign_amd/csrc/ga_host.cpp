@@ -405,7 +405,7 @@ struct ga_ctx {
     int walk_waits = 0, walk_tiles = 0, walk_t_tile = 0, walk_t_ring = 0, walk_t_total = 0, walk_c_total = 0, walk_load_ticks = 0, walk_load_count = 0;
     DevBuf dbg, wdbg;
     // the recompute walk: the score fill's checkpoints, the tile cache, the blocks' flags
-    DevBuf colck, stck, rc_tb, rc_flags, rc_pos;
+    DevBuf colck, stck, rc_tb, rc_flags, rc_pos, rc_own;
     DevBuf qprof;  // the lane fill's query profile (ga::launch_lane_qprof), rebuilt by every lane fill
     int walk_jump_diag[3] = {0, 0, 0};  // the tie-to-tie walk's trips, region re-checks, ties (result[12..14])
     DevBuf jlut;           // the jump workers' LUT for gap open jlut_o (ga::jump_lut_build)
@@ -1340,9 +1340,13 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     // (+ one 64-column stripe of slack: a loader reads whole 1 KiB runs)
     else HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4));
     const size_t nflags = (size_t)nbi * nbs;
-    if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_epoch >= 0x7ffffff0u) {
+    // the cache slots' owner tags (ga::rc_slot_tag) carry the epoch's ready value: cleared with the flags
+    const size_t nown = (size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * sizeof(unsigned long long);
+    if (c->rc_flags.cap < nflags * sizeof(unsigned) || c->rc_own.cap < nown || c->rc_epoch >= 0x7ffffff0u) {
         HIPCHK(c->rc_flags.ensure(nflags * sizeof(unsigned)));
         HIPCHK(hipMemsetAsync(c->rc_flags.p, 0, c->rc_flags.cap, wb.stream));
+        HIPCHK(c->rc_own.ensure(nown));
+        HIPCHK(hipMemsetAsync(c->rc_own.p, 0, nown, wb.stream));
         c->rc_epoch = 0;
     }
     c->rc_epoch++;
@@ -1357,6 +1361,7 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     if (const char* e = c->xknob("GA_RC_LOADERS")) w.nloaders = std::max(12, std::min(14, atoi(e)));
     w.rc_flags = c->rc_flags.as<unsigned>();
     w.rc_ready = 2u * c->rc_epoch + 1u;
+    w.rc_own = c->rc_own.as<unsigned long long>();
     w.rc_nbs = nbs;
     w.rc_td = TD;
     w.rc_pos = c->rc_pos.as<unsigned>();
@@ -1382,6 +1387,8 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     r.nbs = nbs;
     r.flags = c->rc_flags.as<unsigned>();
     r.epoch = c->rc_epoch;
+    r.own = w.rc_own;
+    if (const char* e = c->knob("GA_RC_TAG_FAULT")) r.tag_fault = std::max(0, atoi(e));
     r.pos = c->rc_pos.as<unsigned>();
     r.tile0 = (int)((((st.i - 1) / 64) << 16) | ((st.j - c->col0 - 1) / 64));  // the walk's first tile
     r.worker_bytes = c->rc_jump ? ga::rc_jump_worker_bytes_host(TD, r.stck_every) : ga::rc_worker_bytes(TD, CB, r.stck_every);
@@ -2344,7 +2351,7 @@ void ga_ctx_destroy(ga_ctx* c) {
     for (DevBuf* b : {&c->a, &c->b, &c->sub, &c->gh, &c->gv, &c->qp, &c->GVp, &c->GHp, &c->top, &c->left, &c->bnd_row,
                       &c->bnd_col, &c->meta, &c->hand, &c->flags, &c->tb, &c->out_last, &c->full, &c->rng, &c->ops,
                       &c->result, &c->halo_in, &c->dbg, &c->wdbg, &c->bscr, &c->ckpt, &c->colck, &c->stck,
-                      &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->link, &c->qprof})
+                      &c->rc_tb, &c->rc_flags, &c->rc_pos, &c->rc_own, &c->link, &c->qprof})
         b->release();
     if (c->prog_host) (void)hipHostFree(c->prog_host);
     if (c->peer_link) (void)hipIpcCloseMemHandle(c->peer_link);

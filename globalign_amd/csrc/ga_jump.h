@@ -193,12 +193,12 @@ __device__ __forceinline__ void walk_jump_body(const WalkArgs& w, const uint32_t
                     const int sl = li + JNLOAD * q, tti = tg >> 16, ttj = tg & 0xffff;
                     if (sgpr(__hip_atomic_load(&jtag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
                     // only once the tile's block has been recomputed (its entries are then in the cache)
-                    if (sgpr((int)g_ld(w.rc_flags + (long long)(tti >> 1) * w.rc_nbs + ttj / (2 * w.rc_td))) != (int)w.rc_ready)
-                        continue;
+                    if (!rc_slot_ok(w, tti >> 1, ttj / (2 * w.rc_td), true)) continue;
                     if (lane == 0) __hip_atomic_store(&jtag[sl], -1, __ATOMIC_SEQ_CST, WGS);
                     if (!jin_block(sgpr(__hip_atomic_load(&jcur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                     jload_tile(w, tti, ttj, E, lane);
+                    if (!rc_slot_ok(w, tti >> 1, ttj / (2 * w.rc_td), false)) continue;  // its slot changed under the copy
                     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile's LDS stores before its tag
                     if (lane == 0) {
                         atomicAdd(&jload_ticks, __builtin_amdgcn_s_memrealtime() - t0);

@@ -74,7 +74,7 @@ __device__ __forceinline__ void rc_windows(const RcArgs& r, uint32_t* awin, int2
 
 // Recompute block (bi, bs): rows 64*bi+1 .. 64*bi+64 of fill stripe bs, its traceback words into the cache.
 template <int TD, int CB>
-__device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int bi, int bs, int lane) {
+__device__ bool rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int bi, int bs, int lane) {
     const int SP = rc_sp(CB, r.stck_every), AW = rc_aw(r.stck_every);
     uint8_t* stage = wl;                                                  // [64*TD columns][SP]
     uint32_t* awin = reinterpret_cast<uint32_t*>(wl + 64 * TD * SP);  // dword i: a[base+i .. base+i+3]
@@ -191,8 +191,9 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     {
         const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
         const int tile = pv ? (int)(pv - 1u) : r.tile0;
-        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return;  // out of reach: nobody reads it
+        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return false;  // out of reach: nobody reads it
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot's owner tag cleared (rc_server) before any word
 #pragma unroll
     for (int p = 0; p < TD; p++) {
         const uint4* src = reinterpret_cast<const uint4*>(stage + (p * 64 + lane) * SP + (R0 - t0 + 64) * CB);  // row R0+1
@@ -201,6 +202,7 @@ __device__ void rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
 #pragma unroll
         for (int d = 0; d < 4 * CB; d++) st16_sc1(dst + d * 64, src[d]);
     }
+    return true;
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -223,7 +225,7 @@ constexpr int JLUT_OFF = 2048;                 // after the int16 sub' table
 constexpr int JWORK_OFF = JLUT_OFF + 1024 * 16;  // then the workers
 
 template <int TD>
-__device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4* lut, uint8_t* wl, int bi, int bs,
+__device__ bool rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4* lut, uint8_t* wl, int bi, int bs,
                               int lane) {
     static_assert(TD == 1 || TD == 2 || TD == 4, "jump entries: at most 4 columns per lane");
     const int AW = rc_aw(r.stck_every);
@@ -392,8 +394,9 @@ __device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4*
         // (the reach check of rc_block: a block the walker can no longer reach is not written)
         const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
         const int tile = pv ? (int)(pv - 1u) : r.tile0;
-        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return;
+        if (bi > (tile >> 16) || bs * TD > (tile & 0xffff)) return false;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot's owner tag cleared (rc_server) before any word
     // the block's 2 x 2TD tiles of 32 x 32 cells, 6 KB each ([level][32 rows][32 columns], ga_jump.h), into its
     // cache slot with write-through stores
     uint8_t* blk = r.tb + (size_t)((bi % RC_CACHE_I) * RC_CACHE_S + bs % RC_CACHE_S) * (4 * TD * JTILE_BYTES);
@@ -409,6 +412,7 @@ __device__ void rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4*
                 st16_sc1(dst + q * 64, v);
             }
         }
+    return true;
 }
 
 template <int TD, int CB, bool JUMP = false>
@@ -430,7 +434,7 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
     uint8_t* wl = dyn + (JUMP ? JWORK_OFF : 1024) + wave * r.worker_bytes;
     const unsigned claimed = 2u * r.epoch, ready = claimed + 1u;
     const int dbi = r.off[lane] >> 3, dbs = r.off[lane] & 7;
-    unsigned idle = 0;
+    unsigned idle = 0, nblk = 0;
     for (;;) {
         if (sgpr((int)g_ld(r.pos + 1))) break;  // the walk has ended
         const unsigned pv = (unsigned)sgpr((int)g_ld(r.pos));
@@ -453,9 +457,17 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
                                                            __ATOMIC_RELAXED, __ATOMIC_RELAXED, AGENT);
             if (sgpr(won)) {
                 const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-                if constexpr (JUMP) rc_block_jump<TD>(r, stab16, lut, wl, bi_i, bs_i, lane);
-                else rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the flag
+                // the slot's words are about to change: its owner tag cleared first (ga::rc_slot_tag)
+                unsigned long long* const own = r.own + rc_slot(bi_i, bs_i);
+                if (lane == 0) __hip_atomic_store(own, 0ull, RLX, AGENT);
+                bool wrote;
+                if constexpr (JUMP) wrote = rc_block_jump<TD>(r, stab16, lut, wl, bi_i, bs_i, lane);
+                else wrote = rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the tag
+                // (GA_RC_TAG_FAULT: a lost tag, which the walk's loaders must repair through a recompute)
+                const bool fault = r.tag_fault > 0 && ++nblk % (unsigned)r.tag_fault == 0;
+                if (lane == 0 && wrote && !fault) __hip_atomic_store(own, rc_slot_tag(bi_i, bs_i, r.nbs, ready), RLX, AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tag before the flag
                 if (lane == 0) g_st(r.flags + (long long)bi_i * r.nbs + bs_i, ready);
                 if (lane == 0) {  // diagnostics: blocks recomputed, their total time (100 MHz ticks)
                     atomicAdd(r.pos + 2, 1u);

@@ -232,6 +232,29 @@ __device__ __forceinline__ int sgpr(int x) { return __builtin_amdgcn_readfirstla
 constexpr int WALK_WAVES = 16;
 constexpr int NLOAD_MAX = 14;  // loader waves: 12 (default), 13 (+ the idle wave), 14 (+ the prefetcher's)
 
+// The recompute walk's cache slot check (ga::rc_slot_tag): true while block (bi, bs)'s words are in its
+// slot.  A loader asks before it copies a tile (pre) and after the copy has landed; it uses the copy only if both
+// say so.  Before a copy, a block whose flag says ready although its slot's tag differs (the tag is set before the
+// flag, and the second tag read below is issued after the flag read returned) lost its words to another block's
+// worker: its flag is reset, so a worker recomputes it.
+__device__ inline bool rc_slot_ok(const WalkArgs& w, int bi, int bs, bool pre) {
+    unsigned long long* const own = w.rc_own + rc_slot(bi, bs);
+    const unsigned long long want = rc_slot_tag(bi, bs, w.rc_nbs, w.rc_ready);
+    auto tag = [&]() {
+        const unsigned long long t = __hip_atomic_load(own, RLX, AGENT);
+        return ((unsigned long long)sgpr_u((unsigned)(t >> 32)) << 32) | sgpr_u((unsigned)t);
+    };
+    if (!pre) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copy's loads have returned
+    if (tag() == want) return true;
+    if (!pre) return false;  // the next poll decides
+    unsigned* const fl = w.rc_flags + (long long)bi * w.rc_nbs + bs;
+    if (sgpr_u(g_ld(fl)) == w.rc_ready && tag() != want && (threadIdx.x & 63) == 0) {
+        unsigned e = w.rc_ready;
+        __hip_atomic_compare_exchange_strong(fl, &e, 0u, RLX, RLX, AGENT);
+    }
+    return false;
+}
+
 __device__ __forceinline__ bool in_block(int cur, int ti, int tj) {
     const int dti = (cur >> 16) - ti, dtj = (cur & 0xffff) - tj;
     return cur >= 0 && dti >= 0 && dti < TB4 && dtj >= 0 && dtj < TB4;
@@ -417,14 +440,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                     if (tg < 0) continue;
                     const int sl = li + nload * q, tti = tg >> 16, ttj = tg & 0xffff;
                     if (sgpr(__hip_atomic_load(&tag[sl], __ATOMIC_RELAXED, WGS)) == tg) continue;
-                    // RC: only once the tile's block has been recomputed (its words are then in memory)
-                    if (RC && sgpr((int)g_ld(w.rc_flags + (long long)tti * w.rc_nbs + ttj / w.rc_td)) != (int)w.rc_ready)
-                        continue;
+                    // RC: only once the tile's block has been recomputed (its words are then in its cache slot)
+                    if (RC && !rc_slot_ok(w, tti, ttj / w.rc_td, true)) continue;
                     if (lane == 0) __hip_atomic_store(&tag[sl], -1, __ATOMIC_SEQ_CST, WGS);
                     if (!in_block(sgpr(__hip_atomic_load(&cur_tile, __ATOMIC_SEQ_CST, WGS)), tti, ttj)) continue;
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                     if (CB == 1) load_tile_b1<RC>(w, tti, ttj, torus, sa[li], lut, lane);
                     else load_tile<CB, RC>(w, tti, ttj, torus, sa[li], lut, lutF, lane);
+                    if (RC && !rc_slot_ok(w, tti, ttj / w.rc_td, false)) continue;  // its slot changed under the copy
                     if (lane == 0) {
                         atomicAdd(&load_ticks, __builtin_amdgcn_s_memrealtime() - t0);
                         atomicAdd(&load_count, 1);
@@ -759,6 +782,7 @@ __device__ __forceinline__ WalkArgs uniform_walk_args(const WalkArgs& s) {
     w.skip_corners = sgpr(s.skip_corners);
     w.nloaders = sgpr(s.nloaders);
     w.rc_flags = nullptr;
+    w.rc_own = nullptr;
     w.rc_pos = nullptr;
     w.ops_prog = nullptr;
     return w;

@@ -91,6 +91,15 @@ def test_rc_worker_pools_vs_oracle(monkeypatch, env):
     assert kind[1] == 4, kind
 
 
+@pytest.mark.parametrize("jump", [0, 1])
+def test_rc_lost_slot_tags_repaired_vs_oracle(monkeypatch, jump):
+    """Cache slot owner tags (ga::rc_slot_tag, ADVICE r4): every 3rd block a worker writes is left without its tag,
+    as if another block's worker had overwritten the slot; the walk's loaders must never use such a slot, reset the
+    block's ready flag and wait for its recompute, and the alignment stays the oracle's, in both walks."""
+    _align(monkeypatch, splitmix_seq(2200, 45, "dna"), splitmix_seq(2400, 46, "dna"), DNA, seed=45,
+           env={"GA_RC_TAG_FAULT": 3, "GA_RC_JUMP": jump})
+
+
 @pytest.mark.parametrize("o", [7, 130])
 def test_rc_word_widths_vs_oracle(monkeypatch, o):
     """Two- and four-byte traceback words (gap open >= 7, >= 128)."""
