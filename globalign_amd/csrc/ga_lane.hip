@@ -443,10 +443,18 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     // the recompute checkpoints' right edge of this stripe, and a scratch slot per lane past all of them
     int2* const colck_s = RC && p.colck != nullptr ? p.colck + (long long)s * (m + 1 + COLCK_PAD) : nullptr;
     int2* const colck_x = RC && p.colck != nullptr ? colck_s + (m + 1 + lane) : nullptr;
-    // the lean steady state's checkpoint store: the stripe's base in SGPRs and a 32-bit offset per lane, rows
-    // rlo + lane - 48 (lanes 48..63; LEAN sub-chunks hold no row past m) or the lane's scratch slot: off = cb + cm * rlo
-    const unsigned ck_cb = lane >= 48 ? (unsigned)(lane - 48) * 8u : (unsigned)(m + 1 + lane) * 8u;
+    // the lean steady state's checkpoint store: a raw buffer over the stripe's rows (base and size in SGPRs) and a
+    // 32-bit offset per lane, rows rlo + lane - 48 for lanes 48..63 (LEAN sub-chunks hold no row past m), off the
+    // buffer's end for the others, whose stores the buffer's range check then drops: no exec change, and no scratch
+    // writes (they were three quarters of the store's bytes); off = cb + cm * rlo
+    const unsigned ck_cb = lane >= 48 ? (unsigned)(lane - 48) * 8u : 0x7ffffff0u;
     const unsigned ck_cm = lane >= 48 ? 8u : 0u;
+    lk_v4i ck_rsrc = {0, 0, 0, 0};
+    if (RC && p.colck != nullptr) {
+        const unsigned long long cbase = reinterpret_cast<unsigned long long>(colck_s);
+        ck_rsrc = lk_v4i{(int)sgpr_u((unsigned)cbase), (int)(sgpr_u((unsigned)(cbase >> 32)) & 0xffffu),
+                         (int)sgpr_u((unsigned)(m + 1) * 8u), 0x00020000};  // stride 0, num_records, gfx9 dword 3
+    }
     unsigned avail = 0, outfree = 0, qavail = 0;
     bool aborted = false;
     unsigned long long wcyc[3] = {0, 0, 0}, t_start = 0, c_start = 0;
@@ -669,7 +677,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                         // (colck is set whenever the RC variant runs, enqueue_fill) one offset and one store
                         const lk_v2u vv = (lane & 4) ? lk_v2u{(unsigned)R[0], (unsigned)R[1]} : lk_v2u{(unsigned)R[2], (unsigned)R[3]};
                         const unsigned off = ck_cb + ck_cm * (unsigned)rlo;
-                        asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(off), "v"(vv), "s"(colck_s) : "memory");
+                        asm volatile("buffer_store_dwordx2 %1, %0, %2, 0 offen" ::"v"(off), "v"(vv), "s"(ck_rsrc) : "memory");
                     } else if (RC && p.colck != nullptr) {
                         // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge; every lane stores (lanes
                         // without a row into the scratch slots past the checkpoints): no exec change, which would
