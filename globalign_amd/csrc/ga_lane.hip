@@ -491,6 +491,23 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     const unsigned ca_lds = lds_addr(prod_in);
     const unsigned pq_lds = lds_addr(pq);
     const unsigned scr_lds = lds_addr(smem + LK_SCR_OFF);
+    // ... and their loop-invariant per-lane parts, so that a sub-chunk's addresses cost one op each (round 5: the
+    // compiler's forms took 27 instructions between two lean statements): the profile rows q4[k] + ((4 r - 4 lane) &
+    // 4 qmask); the edge rows (ea_s & ea_m) | ea_b (lane 0 the ring's rows, the others the zero block); the row stores
+    // ((8 x + 8 lane) & w?_m) + w?_b (lanes 48..63 their ring slot, the others a scratch slot of their own)
+    unsigned q4[TD], ea_m, ea_b, wa_m, wa_b, wb_m, wb_b;
+    {
+#pragma unroll
+        for (int k = 0; k < TD; k++) q4[k] = pq_lds + 4u * qb[k];
+        const unsigned scr = scr_lds + 8u * (unsigned)lane, rout_l = lds_addr(rin + RING);
+        const bool hi = lane >= 48;
+        ea_m = lane == 0 ? ~0u : 0u;
+        ea_b = lane == 0 ? 0u : lds_addr(ezero);
+        wa_m = hi && (lane & 4) ? 8u * RMASK : 0u;
+        wa_b = hi && (lane & 4) ? rout_l : scr;
+        wb_m = hi && !(lane & 4) ? 8u * RMASK : 0u;
+        wb_b = hi && !(lane & 4) ? rout_l : scr;
+    }
     {
         const int4* src = lane == 0 ? reinterpret_cast<const int4*>(rin) : ezero;
 #pragma unroll
@@ -632,16 +649,19 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                     lk_v4i Ev[NE];
 #pragma unroll
                     for (int k = 0; k < NE; k++) Ev[k] = lk_v4i{C[k].x, C[k].y, C[k].z, C[k].w};
-                    const unsigned ea = lane == 0 ? lds_addr(rin + ((r0 + SUB) & RMASK)) : lds_addr(ezero);
-                    const unsigned qi = (unsigned)(r0 + SUB - lane) & qmask;
-                    unsigned qbv[TD];
+                    // (the invariant parts above; the asm forms keep the compiler from re-deriving them)
+                    unsigned ea, qi4, wt, wa, wb, qbv[TD];
+                    const unsigned ea_s = lds_addr(rin) + 8u * ((unsigned)(r0 + SUB) & RMASK);
+                    asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(ea) : "s"(ea_s), "v"(ea_m), "v"(ea_b));
+                    asm volatile("v_sub_u32 %0, %1, %2" : "=v"(qi4) : "s"(4u * (unsigned)(r0 + SUB)), "v"(4u * (unsigned)lane));
+                    qi4 &= 4u * qmask;
 #pragma unroll
-                    for (int k = 0; k < TD; k++) qbv[k] = pq_lds + 4u * (qb[k] + qi);
-                    const unsigned slot = rout_lds + 8u * ((unsigned)(rlo - 1 + lane - 48) & RMASK);
-                    const unsigned scr = scr_lds + 8u * (unsigned)lane;
+                    for (int k = 0; k < TD; k++) asm volatile("v_add_u32 %0, %1, %2" : "=v"(qbv[k]) : "v"(q4[k]), "v"(qi4));
+                    asm volatile("v_add_u32 %0, %1, %2" : "=v"(wt) : "s"(8u * (unsigned)(rlo - 49)), "v"(8u * (unsigned)lane));
+                    wa = (wt & wa_m) + wa_b;
+                    wb = (wt & wb_m) + wb_b;
+                    const unsigned wc = lane == 0 ? pc_lds : scr_lds + 8u * (unsigned)lane;
                     const bool hi = lane >= 48;
-                    const unsigned wa = hi && (lane & 4) ? slot : scr, wb = hi && !(lane & 4) ? slot : scr;
-                    const unsigned wc = lane == 0 ? pc_lds : scr;
                     const lk_v2u cp = {(unsigned)(r0 + 2 * SUB), (unsigned)max(rlo + SUB - 1, 0)};
                     unsigned cv;
                     lk_v4i En[NE];

@@ -1,7 +1,7 @@
 set -o pipefail
 # round 5: the chain head of the lane fills (stripe 0 and every workgroup's first stripe): duration, busy cycles per step
 # and what it waited for -- C3 shape at TD 4 (the recompute fill's width), C4 (TD 8, two rounds), 1M x 125k (slab at N=8)
-O=gpurun_out/r5_lean
+O=gpurun_out/r5_head
 mkdir -p $O
 run() {
   name=$1; shift
@@ -10,8 +10,8 @@ run() {
 import json, sys
 import numpy as np
 name, m = sys.argv[1], int(sys.argv[2])
-st = np.load(f"gpurun_out/r5_lean/raw_{name}.npy").astype(np.int64)
-d = json.loads(open(f"gpurun_out/r5_lean/stamps_{name}.json").read().strip().splitlines()[-1])
+st = np.load(f"gpurun_out/r5_head/raw_{name}.npy").astype(np.int64)
+d = json.loads(open(f"gpurun_out/r5_head/stamps_{name}.json").read().strip().splitlines()[-1])
 t0 = st[:, 0].min(); tot = np.maximum(st[:, 5], 1)
 dur = (st[:, 1] - st[:, 0]) / 100.0
 busy = (tot - st[:, 2] - st[:, 3] - st[:, 4]) / (m + 63)
