@@ -79,12 +79,12 @@ MULTI_GPU_DEFAULT = "c4"
 # instructions per fill launch, the fill kernel's static VALU mix, the VALU issue microbenchmark
 # (C3: the pipeline's lane-skewed traceback fill, fill_lane_kernel<4,4,1,8>; C4: the lane-skewed
 # score fill fill_lane_kernel<4,8,0,16>)
-# (round 4, tools/profile_r04.sh: every workload's fill from this tree -- C3 the recompute walk's checkpointing lane
-# fill fill_lane_kernel<4,2,0,16,...,RC>, C4 the score-only lane fill fill_lane_kernel<4,8,0,16>, C5 / C2 the row-scan
-# fill with traceback words fill_kernel<2|1,...>)
-TRAFFIC_FILES = {w: f"r04/traffic_{w}.json" for w in ("c3", "c4", "c5", "c2")}
-VALU_FILES = {w: f"r04/valu_{w}.json" for w in ("c3", "c4", "c5", "c2")}
-VALU_MIX_FILES = {w: f"r04/valu_mix_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+# (round 5, tools/profile_r05.sh on the round-5 fills: C3 / C5 / C2 the recompute walk's checkpointing lane fill
+# fill_lane_kernel<4,4,0,16,...,RC,LATE>, C4 the score-only lane fill fill_lane_kernel<4,8,0,16>; the mixes from
+# tools/lane_variant_asm.sh + tools/valu_mix.py --asm-block-with v_min3_i32)
+TRAFFIC_FILES = {w: f"r05/traffic_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+VALU_FILES = {w: f"r05/valu_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+VALU_MIX_FILES = {w: f"r05/valu_mix_{w}.json" for w in ("c3", "c4", "c5", "c2")}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
 
