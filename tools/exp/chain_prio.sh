@@ -1,3 +1,5 @@
+# STALE: the knobs this script sets were removed from ga_host.cpp in round 4, so it now measures the
+# default path; kept only as the record of the measurement DESIGN.md cites.
 # round 2: the walk chain's stream priority (least / normal / greatest) against per-walk launches: C5 / C3
 set -o pipefail
 mkdir -p gpurun_out/exp

@@ -1,3 +1,5 @@
+# STALE: the knobs this script sets were removed from ga_host.cpp in round 4, so it now measures the
+# default path; kept only as the record of the measurement DESIGN.md cites.
 # round 2: walk chain with fill 0 alone on the chip before the other fills (GA_CHAIN_STAGGER=1) / all at once
 set -o pipefail
 mkdir -p gpurun_out/exp

@@ -1,3 +1,5 @@
+# STALE: the knobs this script sets were removed from ga_host.cpp in round 4, so it now measures the
+# default path; kept only as the record of the measurement DESIGN.md cites.
 # Round 3: what the recompute checkpoints cost the C3 fill (timing only: the walks of the DBG runs are wrong)
 set -o pipefail
 mkdir -p gpurun_out
