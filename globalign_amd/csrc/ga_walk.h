@@ -678,10 +678,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                 }
             }
             ops = (ops << 8) | (A >> 3);
-            const unsigned mv = (ix - rel) & 0xffu;
+            // the next group starts at this group's net move, unmasked (round 5): its low byte is the moves (no carry out
+            // of it: at most 36 + 36), the upper bytes only this group's index-advance carries, which the readlane
+            // ignores as it does inside a group; the mask is off the chain, for the bookkeeping
+            const unsigned nrel = ix - rel, mv = nrel & 0xffu;
             i -= (int)(mv >> 3);
             j -= (int)(mv & 7u);
-            rel = mv;
+            rel = nrel;
             // the widening above stays in this group (scheduled past the boundary it put six VALU ahead of
             // the next group's first readlane)
             __builtin_amdgcn_sched_barrier(0);
