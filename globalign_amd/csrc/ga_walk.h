@@ -276,6 +276,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
     asm volatile("" : "+v"(tid));
     __shared__ __attribute__((aligned(16))) uint32_t rngbuf[RB];
     __shared__ uint32_t opsbuf[RB / 16];
+    __shared__ uint32_t ops_dummy;  // where the walker's deferred level-word store goes when none is pending
     __shared__ uint16_t lut[256];
     __shared__ uint8_t lutF[128];
     __shared__ __attribute__((aligned(16))) uint8_t sa[NLOAD_MAX][TT];
@@ -639,7 +640,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
 
         // One group of 4 steps: swap in the prefetched window and entries, prefetch the next ones.
         // CHECK: stop at the matrix edge; returns the steps taken when the walk ended, else 0.
-        auto group = [&](auto check_tag, int gd) -> int {  // gd: dispatch of the group's first step
+        // hook: work of the iteration's bookkeeping, placed in the group's scheduling region so that it issues in the
+        // shadows of the chain's readlanes (in-order issue: at the loop boundary every instruction sat on the chain)
+        auto group = [&](auto check_tag, int gd, auto hook) -> int {  // gd: dispatch of the group's first step
             constexpr bool CHECK = decltype(check_tag)::value;
             const int wcur = wcw;
             const uint4 tc = tnext;
@@ -649,6 +652,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             wnext = window(i, j);
             tnext = tabs(gd + 4);
             __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
+            hook();
             const unsigned t[4] = {(unsigned)sgpr((int)tc.x), (unsigned)sgpr((int)tc.y), (unsigned)sgpr((int)tc.z),
                                    (unsigned)sgpr((int)tc.w)};
             // ix: the readlane index.  Only its low 6 bits count, so the moves go in unmasked; its low
@@ -690,6 +694,18 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             __builtin_amdgcn_sched_barrier(0);
             return 0;
         };
+        // The iteration boundary, software-pipelined (round 5): an iteration's level word is stored during the next
+        // one's first group, and whether the next iteration needs any test (a level block to start, tiles to verify,
+        // the matrix edge) is decided during its third group from bounds (two groups move at most 8 rows and 8
+        // columns); a fast iteration then follows with one branch.  The pending word goes out before any slow path.
+        uint32_t* ops_slot = &ops_dummy;
+        unsigned ops_pend = 0;
+        bool fast;
+        auto no_hook = []() {};
+        auto flush_ops = [&]() {
+            *ops_slot = ops_pend;
+            ops_slot = &ops_dummy;
+        };
         for (;;) {
             // iteration of 16 dispatches D .. D+15 (D % 16 == 0)
             if constexpr (SLD) {
@@ -697,23 +713,37 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                 asm volatile("" : "+s"(rng_it));  // the address in SGPRs (no vector induction variable)
                 d_it = D;
             }
+            flush_ops();
             if ((D & 511) == 0) block_start(D);
             if (!SLD && ((D + 16) & 511) == 0) rng_ready(D + 16);
             // every window of this iteration is anchored within 12 steps: rows >= i - 19
             if (__builtin_expect(i - 19 < vlo_i || j - 19 < vlo_j, 0)) verify(i, j);
             if (__builtin_expect(min(i, j) > 16, 1)) {
-                group(std::false_type{}, D);
-                group(std::false_type{}, D + 4);
-                group(std::false_type{}, D + 8);
-                group(std::false_type{}, D + 12);
-                opsbuf[(D >> 4) & (RB / 16 - 1)] = ops;
-                D += 16;
+                // fast iterations back to back: one branch between them
+                do {
+                    if constexpr (SLD) {
+                        rng_it = rng_s + D;
+                        asm volatile("" : "+s"(rng_it));
+                        d_it = D;
+                    }
+                    const int dn = D + 16;
+                    group(std::false_type{}, D, [&]() { *ops_slot = ops_pend; });
+                    group(std::false_type{}, D + 4, no_hook);
+                    group(std::false_type{}, D + 8, [&]() {
+                        fast = (dn & 511) != 0 && (SLD || ((dn + 16) & 511) != 0) && min(i, j) > 24 &&
+                               i - 27 >= vlo_i && j - 27 >= vlo_j;
+                    });
+                    group(std::false_type{}, D + 12, no_hook);
+                    ops_slot = &opsbuf[(D >> 4) & (RB / 16 - 1)];
+                    ops_pend = ops;
+                    D = dn;
+                } while (__builtin_expect(fast, 1));
                 continue;
             }
             // near the top / left edge (the verified tiles reach row / column 1 here)
             int g = 0, k = 0;
             for (; g < 4; g++) {
-                k = group(std::true_type{}, D + 4 * g);
+                k = group(std::true_type{}, D + 4 * g, no_hook);
                 if (k) break;
             }
             if (g < 4) {
