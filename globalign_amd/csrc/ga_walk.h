@@ -649,10 +649,6 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             // SLD: wait for this group's entries (loaded a group ago) before the new LDS / scalar loads go
             // out, so that the wait does not also cover them
             if constexpr (SLD) asm volatile("" ::"s"(tc.x), "s"(tc.y), "s"(tc.z), "s"(tc.w));
-            wnext = window(i, j);
-            tnext = tabs(gd + 4);
-            __builtin_amdgcn_sched_barrier(0);  // issue the prefetch here, not where the next group needs it
-            hook();
             const unsigned t[4] = {(unsigned)sgpr((int)tc.x), (unsigned)sgpr((int)tc.y), (unsigned)sgpr((int)tc.z),
                                    (unsigned)sgpr((int)tc.w)};
             // ix: the readlane index.  Only its low 6 bits count, so the moves go in unmasked; its low
@@ -662,6 +658,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const unsigned v = (unsigned)__builtin_amdgcn_readlane(wcur, (int)ix);
+                if (k == 0) {
+                    // the next group's window and entries, issued in the first readlane's shadow (round 5: issued
+                    // before it they sat on the chain), not where the next group needs them
+                    __builtin_amdgcn_sched_barrier(0);
+                    wnext = window(i, j);
+                    tnext = tabs(gd + 4);
+                    __builtin_amdgcn_sched_barrier(0);
+                    hook();
+                }
                 // widen the next group's window (read at this group's start) while the last step's
                 // scalar chain runs
                 if (k == 3) wcw = widen(wnext);
