@@ -633,7 +633,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
         verify(i, j);
         int wnext = window(i, j);    // anchored at the walk's current cell
         int wcw = widen(wnext);      // the next group's window, widened (off the next group's chain)
-        uint4 tnext = tabs(D);
+        uint4 tnext = tabs(D), tnext2 = tabs(D + 4);  // the entries of the next two groups
         unsigned rel = 0;            // offset of the current cell from wnext's anchor (di*8 + dj)
         unsigned L8 = 8u * L;        // bit offset of the entering level's field in a window cell
         unsigned ops = 0;
@@ -646,6 +646,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
             constexpr bool CHECK = decltype(check_tag)::value;
             const int wcur = wcw;
             const uint4 tc = tnext;
+            tnext = tnext2;
             // SLD: wait for this group's entries (loaded a group ago) before the new LDS / scalar loads go
             // out, so that the wait does not also cover them
             if constexpr (SLD) asm volatile("" ::"s"(tc.x), "s"(tc.y), "s"(tc.z), "s"(tc.w));
@@ -663,13 +664,19 @@ __device__ __forceinline__ void walk_body(const WalkArgs& w, const uint32_t* rng
                     // before it they sat on the chain), not where the next group needs them
                     __builtin_amdgcn_sched_barrier(0);
                     wnext = window(i, j);
-                    tnext = tabs(gd + 4);
                     __builtin_amdgcn_sched_barrier(0);
                     hook();
                 }
                 // widen the next group's window (read at this group's start) while the last step's
                 // scalar chain runs
-                if (k == 3) wcw = widen(wnext);
+                if (k == 3) {
+                    wcw = widen(wnext);
+                    // the entries of the group after next, loaded once the widening's wait is behind (scalar loads
+                    // return out of order, so a load in flight there made that wait cover it too)
+                    __builtin_amdgcn_sched_barrier(0);
+                    tnext2 = tabs(gd + 8);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 // the chosen level comes out as the next field's bit offset (lvl * 8): two dependent
                 // scalar ops fewer per step than extracting lvl and scaling it
                 L8 = (t[k] >> ((v >> L8) & 31u)) & 0x18u;
