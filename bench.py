@@ -428,7 +428,14 @@ def main():
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C4 point of the N=1 line")
+    ap.add_argument("--opt", action="append", default=[], metavar="GA_NAME=VALUE",
+                    help="a context option (ga_ctx_create_opts: kernel variants for experiments); repeatable")
     args = ap.parse_args()
+    if args.opt:
+        from globalign_amd import _native
+        for kv in args.opt:
+            k, _, v = kv.partition("=")
+            _native.OPTIONS[k] = v
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

@@ -40,7 +40,7 @@ class EngineError(RuntimeError):
 
 # every symbol include/globalign_amd.h declares (tests check the exports)
 EXPORTS = [
-    "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_destroy", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
+    "ga_last_error", "ga_device_count", "ga_ctx_create", "ga_ctx_create_opts", "ga_ctx_destroy", "ga_build_flags", "ga_problem_set", "ga_problem_fill", "ga_problem_set_cells",
     "ga_problem_traceback", "ga_problem_align", "ga_problem_align_many", "ga_problem_set_slab", "ga_slab_buffers", "ga_slab_bind_halos",
     "ga_slab_link", "ga_slab_link_export", "ga_slab_link_import", "ga_enable_peer_access",
     "ga_slab_fill_launch", "ga_slab_fill_finish", "ga_slab_walk_prepare", "ga_slab_walk", "ga_slab_mt_state",
@@ -98,6 +98,8 @@ def load_library():
         L.ga_last_error.restype = C.c_char_p
         L.ga_device_count.argtypes = [C.POINTER(C.c_int)]
         L.ga_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+        L.ga_ctx_create_opts.argtypes = [C.c_int, C.c_char_p, C.POINTER(vp)]
+        L.ga_build_flags.argtypes = [p32]
         L.ga_ctx_destroy.argtypes = [vp]
         L.ga_ctx_destroy.restype = None
         L.ga_problem_set.argtypes = [vp, C.c_char_p, i64, C.c_char_p, i64, C.POINTER(GaCosts), p32, p32]
@@ -148,6 +150,14 @@ def _check(rc):
 PROG_ABORT = 0xFFFFFFFF
 
 
+def experiments_build():
+    """True for a library built with make EXPERIMENTS=1 (the measured-and-dropped paths compiled in)."""
+    L = load_library()
+    f = (C.c_int32 * 1)()
+    _check(L.ga_build_flags(f))
+    return bool(f[0] & 1)
+
+
 def device_count():
     L = load_library()
     n = C.c_int(0)
@@ -179,16 +189,28 @@ class CostTables:
         return bytes(code[ch] for ch in seq)
 
 
+# Explicit context options (ga_ctx_create_opts): kernel variants for tests and tuning, fault injection,
+# diagnostics.  The library reads only its shipped GA_* knobs from the environment; everything
+# else is given here, e.g. OPTIONS["GA_LANE_ASM"] = "0", or per engine through Engine(options=...).
+OPTIONS = {}
+
+
+def options_string(options=None):
+    merged = dict(OPTIONS)
+    merged.update(options or {})
+    return ";".join(f"{k}={v}" for k, v in sorted(merged.items()))
+
+
 class Engine:
     """One HIP device context (ga_ctx)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, options=None):
         L = load_library()
         if device_count() < 1:
             raise EngineError("no HIP device visible: the globalign_amd engine runs on MI355X (gfx950) only")
         self._L = L
         h = C.c_void_p()
-        _check(L.ga_ctx_create(int(device), C.byref(h)))
+        _check(L.ga_ctx_create_opts(int(device), options_string(options).encode(), C.byref(h)))
         self._h = h
         self.device = device
         self.m = self.n = 0
@@ -411,10 +433,11 @@ _default_lock = threading.Lock()
 
 
 def knob_fingerprint():
-    """The GA_* overrides as the environment holds them now.  A context reads them once, when it is created
-    (ga_ctx_create), so cached engines are keyed by them: changing one (tests, tuning) gets a fresh context,
-    and a context's kernel choices never change under it."""
-    return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("GA_")))
+    """The GA_* overrides as the environment and OPTIONS hold them now.  A context reads them once, when it is
+    created (ga_ctx_create_opts), so cached engines are keyed by them: changing one (tests, tuning) gets a fresh
+    context, and a context's kernel choices never change under it."""
+    return (tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("GA_"))),
+            tuple(sorted((k, str(v)) for k, v in OPTIONS.items())))
 
 
 def evict_stale(cache, key):

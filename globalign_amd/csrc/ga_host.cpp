@@ -28,6 +28,8 @@
 #include "../../include/globalign_amd.h"
 #include "ga_device.h"
 #include "ga_lane.h"
+#include "ga_check.h"
+#include "ga_rng.h"
 
 namespace {
 
@@ -69,250 +71,35 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-// ------------------------------------------------------------------ CPython MT19937
-constexpr int MTN = 624, MTM = 397;
-
-struct PyMT {
-    uint32_t mt[MTN];
-    int mti;
-    // one MT19937 twist, branch-free and in three runs without loop-carried dependences the
-    // compiler cannot vectorise (kk+1 is read before it is written; kk-227 was written long before)
-    static inline uint32_t tw(uint32_t a, uint32_t b, uint32_t c) {
-        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-        return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-    }
-    void twist() {
-        uint32_t* __restrict m = mt;
-        for (int kk = 0; kk < MTN - MTM; kk++) m[kk] = tw(m[kk], m[kk + 1], m[kk + MTM]);
-        for (int kk = MTN - MTM; kk < MTN - 1; kk++) m[kk] = tw(m[kk], m[kk + 1], m[kk + (MTM - MTN)]);
-        m[MTN - 1] = tw(m[MTN - 1], m[0], m[MTM - 1]);
-        mti = 0;
-    }
-    inline uint32_t next() {
-        if (mti >= MTN) twist();
-        uint32_t y = mt[mti++];
-        y ^= (y >> 11);
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= (y >> 18);
-        return y;
-    }
-    // random.choice(seq of len n) for n in {2,3}: getrandbits(2) with rejection
-    inline unsigned below(unsigned n) {
-        unsigned r;
-        do { r = next() >> 30; } while (r >= n);
-        return r;
-    }
-};
-
-// ---------------------------------------------------------------- tie-break table
-// The dispatcher's 18 draws per step consume a variable number of MT words
-// (getrandbits(2) with rejection: r >= size -> draw again).  The scan below
-// turns the word stream into the stream of ACCEPTED draws (18 per step) four
-// words at a time through a table indexed by (draw index mod 18, top-2-bit
-// quartet), then builds each step's entry from draws 0-3 / 9-12.
-struct QuadEntry {
-    uint32_t bytes;  // accepted values, one per byte, in order (unused bytes 0)
-    uint16_t meta;   // nacc (3 bits) | word offset of each acceptance (4 x 2 bits) << 3
-};
-struct Quad {
-    QuadEntry e[18][256];
-    Quad() {
-        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
-        for (int d = 0; d < 18; d++)
-            for (int B = 0; B < 256; B++) {
-                unsigned dd = d, nacc = 0, bytes = 0, pos = 0;
-                for (unsigned wi = 0; wi < 4; wi++) {
-                    const unsigned r = (B >> (2 * wi)) & 3u;
-                    if (r < sz[dd]) {
-                        bytes |= r << (8 * nacc);
-                        pos |= wi << (2 * nacc);
-                        nacc++;
-                        dd = (dd + 1) % 18;
-                    }
-                }
-                e[d][B].bytes = bytes;
-                e[d][B].meta = (uint16_t)(nacc | (pos << 3));
-            }
-    }
-};
-
-// Branch-free form of the same table: next draw index, whether a dispatch completes inside the
-// quartet and the word offset (+1) of its 18th acceptance.
-struct QuadEntry2 {
-    uint32_t bytes;
-    uint8_t nacc, nd, wrap, woff;
-};
-struct Quad2 {
-    QuadEntry2 e[18][256];
-    Quad2() {
-        static const Quad Q;
-        for (int d = 0; d < 18; d++)
-            for (int B = 0; B < 256; B++) {
-                const QuadEntry& q = Q.e[d][B];
-                const unsigned nacc = q.meta & 7u;
-                QuadEntry2& r = e[d][B];
-                r.bytes = q.bytes;
-                r.nacc = (uint8_t)nacc;
-                r.nd = (uint8_t)((d + nacc) % 18);
-                r.wrap = (uint8_t)(d + nacc >= 18);
-                r.woff = r.wrap ? (uint8_t)(((q.meta >> (3 + 2 * (17 - d))) & 3u) + 1) : 0;
-            }
-    }
-};
-
-struct RngTable;
-void fill_entries(const uint8_t* acc, int64_t from, int64_t to, RngTable& R);
-
-constexpr int TWSNAP = 64;
-
-inline void temper_block(const uint32_t* mt, uint32_t* out) {
-    for (int k = 0; k < MTN; k++) {
-        uint32_t y = mt[k];
-        y ^= (y >> 11);
-        y ^= (y << 7) & 0x9d2c5680u;
-        y ^= (y << 15) & 0xefc60000u;
-        y ^= (y >> 18);
-        out[k] = y;
-    }
-}
-
-// The tie-break table as a RESUMABLE stream over CPython's MT19937 words: extend(D) makes the
-// entries of dispatches [0, D) available, continuing where the last call stopped.  Consecutive
-// alignments (each a find_global_alignment call that starts from the state the previous one left)
-// consume ONE continuous stream of accepted draws, 18 per dispatch, so alignment k's dispatches are
-// the global dispatches [G_k, G_k + D_k) of the same table (ga_problem_align_many).
-struct RngTable {
-    std::vector<uint32_t> tab;        // per dispatch: level per candidate set (see fill_entries)
-    std::vector<uint32_t> step_end;   // words consumed after each dispatch
-    std::vector<PyMT> twist_snap;     // MT array after every 64th twist (index 0 = initial state)
-    int mti0 = 0;
-    // stream position
-    PyMT g{};
-    uint32_t words[MTN + 4]{};
-    int q = 0, count = 0;             // next word of the current tempered block, words in it
-    int64_t wbase = 0, ntw = 0, p = 0, stp = 0;
-    unsigned d = 0;                   // draw index within the dispatch (0..17)
-    std::vector<uint8_t> acc;         // accepted draws (values 0..2)
-    int64_t built = 0;                // dispatches whose entries are in tab
-
-    void start(const uint32_t* state) {
-        std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
-        g.mti = (int)state[MTN];
-        mti0 = g.mti;
-        twist_snap.assign(1, g);
-        tab.clear();
-        step_end.clear();
-        acc.clear();
-        wbase = ntw = p = stp = built = 0;
-        d = 0;
-        // the partial first block: words mti0 .. 623 of the initial array
-        uint32_t tmp[MTN];
-        temper_block(g.mt, tmp);
-        const int first = g.mti >= MTN ? 0 : g.mti;
-        count = g.mti >= MTN ? 0 : MTN - g.mti;
-        std::memcpy(words, tmp + first, sizeof(uint32_t) * count);
-        q = 0;
-    }
-
-    void extend(int64_t steps) {
-        if (steps <= built) return;
-        static const Quad2 Q;
-        static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
-        const int64_t need = 18 * steps;
-        acc.resize(need + 8);
-        step_end.resize(steps + 4);
-        while (p < need) {
-            if (q >= count) {
-                wbase += count;
-                g.twist();
-                ntw++;
-                if (ntw % TWSNAP == 0) twist_snap.push_back(g);
-                temper_block(g.mt, words);
-                count = MTN;
-                q = 0;
-            }
-            for (; q + 4 <= count && p < need; q += 4) {
-                const unsigned B = (words[q] >> 30) | ((words[q + 1] >> 30) << 2) | ((words[q + 2] >> 30) << 4) |
-                                   ((words[q + 3] >> 30) << 6);
-                const QuadEntry2& e = Q.e[d][B];
-                std::memcpy(acc.data() + p, &e.bytes, 4);
-                step_end[stp] = (uint32_t)(wbase + q + e.woff);  // branch-free: kept only when a dispatch completes
-                stp += e.wrap;
-                p += e.nacc;
-                d = e.nd;
-            }
-            // tail words of the block (count not a multiple of 4), one at a time
-            for (; q + 4 > count && q < count && p < need; q++) {
-                const unsigned r = words[q] >> 30;
-                if (r < sz[d]) {
-                    acc[p] = (uint8_t)r;
-                    if (d == 17) step_end[stp++] = (uint32_t)(wbase + q + 1);
-                    p++;
-                    d = d == 17 ? 0 : d + 1;
-                }
-            }
-        }
-        tab.resize(steps);
-        fill_entries(acc.data(), built, steps, *this);
-        built = steps;
-    }
-};
-
-// The per-step entries from the accepted draws (18 per dispatch; draws 0-3 / 9-12 decide).
-void fill_entries(const uint8_t* acc, int64_t from, int64_t to, RngTable& R) {
-    for (int64_t st = from; st < to; st++) {
-        const uint8_t* r = acc + 18 * st;
-        uint32_t e = 0;
-        for (int half = 0; half < 2; half++) {
-            const uint8_t* qq = r + 9 * half;
-            const unsigned lv[8] = {0, 0, 1, qq[1], 2, 2u * qq[2], 1u + qq[3], qq[0]};  // S = 1..7
-            // level of rank set S at bits 2S+1+14*half (ga_kernels.hip, walk layout)
-            for (int S = 1; S <= 7; S++) e |= lv[S] << (2 * S + 1 + 14 * half);
-        }
-        R.tab[st] = e;
-    }
-}
-
-// The table of `steps` dispatches from the 625-word state (MT array + index).  Twisting and
-// tempering the stream is the cost (~9 ms for 2*10^5 dispatches on an EPYC 9575F); it runs
-// while the device fills.  (A producer/consumer split over two threads measured no faster.)
-void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
-    R.start(state);
-    R.extend(steps);
-}
-
-// MT state after the first D dispatches consumed their words.
-void state_after(const RngTable& R, int64_t D, uint32_t* out) {
-    PyMT g = R.twist_snap[0];
-    if (D == 0) {
-        std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
-        out[MTN] = (uint32_t)g.mti;
-        return;
-    }
-    const int64_t W = R.step_end[D - 1];
-    const int64_t first = R.mti0 >= MTN ? 0 : MTN - R.mti0;
-    if (W <= first) {
-        g.mti = R.mti0 + (int)W;
-    } else {
-        const int64_t Wp = W - first;
-        const int64_t tw = (Wp + MTN - 1) / MTN;           // twists needed
-        const int64_t sidx = tw / TWSNAP;
-        g = R.twist_snap[sidx];
-        for (int64_t t = sidx * TWSNAP; t < tw; t++) g.twist();
-        g.mti = (int)(Wp - (tw - 1) * MTN);
-    }
-    std::memcpy(out, g.mt, sizeof(uint32_t) * MTN);
-    out[MTN] = (uint32_t)g.mti;
-}
+using namespace garng;
+static_assert(ga::COLCK_PAD == 64, "rc_rows_fit (ga_check.h) assumes a 64-row pad");
 
 }  // namespace
 
 // ------------------------------------------------------------------ context
+// The GA_* variables the shipped library reads from the environment (INTEGRATION.md lists them): the path choices
+// and budgets an operator may want to set.  Every other option -- kernel variants for tests and tuning, fault
+// injection, diagnostics -- reaches a context only through ga_ctx_create_opts, never from the environment, so a
+// stray variable cannot change a production context's kernels or inject a fault.  An experiments build
+// (make EXPERIMENTS=1) takes every GA_* variable.
+const char* const kEnvKnobs[] = {"GA_RC",           "GA_RC_MIN_CELLS", "GA_RC_BUDGET_MB",      "GA_RC_EVERY",
+                                 "GA_RC_SERVERS",   "GA_TB_BUDGET_MB", "GA_FILL_MODE",         "GA_COLS_PER_LANE",
+                                 "GA_LANE_COLS_PER_LANE", "GA_PIPE_FILLS", "GA_PIPE_CHAIN",    "GA_STREAM_PRIORITY",
+                                 "GA_HALO_SPIN_LIMIT", "GA_PIPE_TRACE"};
+bool env_knob(const std::string& name) {
+#ifdef GA_EXPERIMENTS
+    return name.compare(0, 3, "GA_") == 0;
+#else
+    for (const char* k : kEnvKnobs)
+        if (name == k) return true;
+    return false;
+#endif
+}
+
 struct ga_ctx {
-    // GA_* tuning / diagnostic overrides, snapshotted when the context is created (ga_ctx_create): a context's
-    // kernel choices never change under it, whatever the process does to its environment later.  knob("GA_X")
-    // is getenv's view of GA_X at that moment (nullptr: unset).
+    // GA_* tuning / diagnostic overrides, snapshotted when the context is created (ga_ctx_create_opts): the
+    // environment's shipped knobs (kEnvKnobs) at that moment, then the caller's options.  A context's kernel choices
+    // never change under it, whatever the process does to its environment later (nullptr: unset).
     std::map<std::string, std::string> knobs;
     const char* knob(const char* name) const {
         const auto it = knobs.find(name);
@@ -552,42 +339,14 @@ bool lane_geometry(ga_ctx* c, int64_t ncol, int* qrows_out, bool tb, int force_T
 
 int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, int64_t n_all, const ga_costs* cs,
                  const int32_t* row0, const int32_t* col0, int64_t cb, int64_t ce) {
-    if (!a || !b_all || !cs || !cs->sub || !cs->gap_h || !cs->gap_v) return fail(GA_E_ARG, "null argument");
-    if (m < 1 || n_all < 1) return fail(GA_E_ARG, "sequences must be non-empty");
-    if (cb < 0 || ce > n_all || ce <= cb) return fail(GA_E_ARG, "bad column slab");
+    ProblemShape ps;
+    std::string why;
+    if (int r = check_problem(a, m, b_all, n_all, cs, row0, col0, cb, ce, ps, why)) return fail(r, why);
     const int K = cs->K;
-    if (K < 1 || K > 255) return fail(GA_E_ARG, "alphabet size K must be in [1,255]");
-    if (cs->gap_open < 0) return fail(GA_E_ARG, "gap_open cost must be >= 0");
-    for (int64_t i = 0; i < m; i++)
-        if (a[i] >= K) return fail(GA_E_ARG, "seq_1 code out of range");
-    for (int64_t j = 0; j < n_all; j++)
-        if (b_all[j] >= K) return fail(GA_E_ARG, "seq_2 code out of range");
-    // int32 range guard: every stored value, shifted or not, and
-    // every intermediate (value + o) must stay far from overflow.
-    int64_t maxabs = 0;
-    for (int q = 0; q < K * K; q++) maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->sub[q]));
-    for (int q = 0; q < K; q++) {
-        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_h[q]));
-        maxabs = std::max<int64_t>(maxabs, std::llabs((long long)cs->gap_v[q]));
-    }
-    const int64_t big = ((int64_t)cs->max_cost + 1) * std::max(m, n_all);
-    int64_t bmax = std::llabs(big);
-    if (row0)
-        for (int64_t q = 0; q < 3 * (n_all + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)row0[q]));
-    if (col0)
-        for (int64_t q = 0; q < 3 * (m + 1); q++) bmax = std::max<int64_t>(bmax, std::llabs((long long)col0[q]));
-    const int64_t bound = bmax + (m + n_all + 2) * (3 * maxabs + (int64_t)cs->gap_open);
-    if (4 * bound >= (int64_t)INT32_MAX) return fail(GA_E_RANGE, "problem exceeds the int32 score range of the device path");
-    int64_t subp_max = 0;
-    for (int x = 0; x < K; x++)
-        for (int y = 0; y < K; y++)
-            subp_max = std::max<int64_t>(subp_max,
-                                         std::llabs((long long)cs->sub[x * K + y] - cs->gap_v[x] - cs->gap_h[y]));
-    c->qbytes = subp_max <= 127 ? 1 : subp_max <= 32767 ? 2 : 0;
-    if (!c->qbytes) return fail(GA_E_RANGE, "substitution costs exceed the int16 query profile");
     const int o = cs->gap_open;
-    c->CB = (o + 1) < 8 ? 1 : (o + 1) < 128 ? 2 : (o + 1) < 32768 ? 4 : 0;
-    if (!c->CB) return fail(GA_E_RANGE, "gap_open cost too large for the traceback word");
+    const int64_t big = ps.big;
+    c->qbytes = ps.qbytes;
+    c->CB = ps.CB;
     c->m = m;
     c->n = ce - cb;
     c->n_global = n_all;
@@ -596,7 +355,6 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     c->o = o;
     c->big = (int)big;
     c->custom = row0 != nullptr || col0 != nullptr;
-    if ((row0 == nullptr) != (col0 == nullptr)) return fail(GA_E_ARG, "row0 and col0 must be given together");
     // one stripe (64 columns) per compute wave; a workgroup (one per CU) chains 4 waves (one per
     // SIMD: the fastest rows) when every stripe gets a wave that way, else 8 (two per SIMD)
     set_stripes(c, c->T_req, false, false);
@@ -689,6 +447,26 @@ struct Band {
 };
 
 // Enqueue boundary + query profile + fill.  Does not synchronise.
+#ifdef GA_EXPERIMENTS
+constexpr bool kRcJumpDefault = false;  // the tie-to-tie walk (DESIGN.md 5.9) unless GA_RC_JUMP says otherwise
+#endif
+// the recompute walk's block cache: the word walk's, and (experiments build) the tie-to-tie walk's entries
+inline size_t rc_cache_bytes(bool jump, int TD, int CB) {
+    // (+ one 64-column stripe of slack: a loader reads whole 1 KiB runs)
+    return jump ? (size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * 4 * TD * 6144 + 65536
+                : (size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4;
+}
+// whether the tie-to-tie walk may run (experiments build, GA_RC_JUMP): the checkpoint sizing then budgets its cache
+inline bool rc_jump_requested(const ga_ctx* c) {
+#ifdef GA_EXPERIMENTS
+    const char* e = c->xknob("GA_RC_JUMP");
+    return e ? atoi(e) != 0 : kRcJumpDefault;
+#else
+    (void)c;
+    return false;
+#endif
+}
+
 int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     int every = bd.rc_every > 0 ? bd.rc_every : 64;  // the recompute fill's checkpoint spacing (chosen below)
     if (!c->loaded) return fail(GA_E_STATE, "no problem loaded");
@@ -738,9 +516,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
             const int64_t nck = std::max<int64_t>((m - 1) / e, 1);
             return nck * c->nstripes * (c->T + 1) * 512;
         };
+        // (the walk's block cache as the walk that will run sizes it: ADVICE r5, the jump cache is ~6x the word one)
         auto other_bytes = [&]() {
             return (int64_t)c->nstripes * (m + 1) * 8 +
-                   (int64_t)ga::RC_CACHE_I * ga::RC_CACHE_S * c->T * 64 * 64 * c->CB + ((int64_t)64 << 20);
+                   (int64_t)rc_cache_bytes(rc_jump_requested(c) && c->T <= 4, c->T, c->CB) +
+                   ((int64_t)64 << 20);
         };
         auto fits = [&](int e) {
             return ck_bytes(e) <= std::min(budget, dev_avail - other_bytes()) &&
@@ -1288,6 +1068,7 @@ bool rc_eligible(ga_ctx* c) {
     const int mode = e ? atoi(e) : -1;
     if (mode == 0 || c->slab || c->qbytes != 1 || c->K > 32) return false;
     if (c->m < 256 || c->n < 256) return false;  // (degenerate walks read cells no block ever recomputes)
+    if (!rc_rows_fit(c->m)) return false;         // the lean checkpoint store's 32-bit buffer (ga_check.h)
     if (mode == 1) return true;
     // 2^26 cells and up (round 4): with the lean sub-chunk and 4-column stripes the recompute call beats the
     // stored-words one from C2 up (one call: C2 2.00 -> 1.75-1.77 ms, C5 4.12 -> 3.92, C3 15.73 -> 15.57;
@@ -1301,11 +1082,8 @@ bool rc_eligible(ga_ctx* c) {
 // The checkpoint spacing trades recompute steps for checkpoint memory, (TD + 1) * 512 B per stripe per
 // spacing: chosen with the geometry in enqueue_fill; GA_RC_EVERY (a power of two >= 64; rounded down) fixes it
 int rc_every_req(const ga_ctx* c) {
-    const char* e = c->knob("GA_RC_EVERY");
-    if (!e) return 0;
-    int v = 64;
-    while (2 * v <= atoi(e) && v < (1 << 20)) v *= 2;
-    return v;
+    const char* e = c->knob("GA_RC_EVERY");  // a power of two in [64, 2^20] (checked in ga_ctx_create_opts)
+    return e ? atoi(e) : 0;
 }
 
 // The score-only checkpointing fill of the loaded problem or slab.
@@ -1321,24 +1099,27 @@ int rc_fill(ga_ctx* c) {
 
 // Launch the walk + recompute workgroups from walk state `st` on the walk buffers `wb` (its table already
 // uploaded), after rc_fill.
-constexpr bool kRcJumpDefault = false;  // the tie-to-tie walk (DESIGN.md 5.9) unless GA_RC_JUMP says otherwise
+
+// The tie-to-tie walk (experiments build only: it measured slower than the word walk, 7.15-7.72
+// against 5.2 ms at C3) when GA_RC_JUMP asks for it and its workers fit: at most 4 columns per lane (a worker stages
+// its block's 3 x 64 x 64*TD entries in LDS) and o <= 14 (X'-H', Y'-H' saturated at o+1 index a 1024-entry LUT).
+bool rc_jump_wanted(ga_ctx* c, int TD) {
+#ifdef GA_EXPERIMENTS
+    return rc_jump_requested(c) && TD <= 4 && c->o <= 14 &&
+           ga::rc_jump_lds_bytes(TD, c->rc_every_used) + 12 * 1024 <= 160 * 1024;
+#else
+    (void)c;
+    (void)TD;
+    return false;
+#endif
+}
 
 int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     const int64_t m = c->m, n = c->n;
     const int TD = c->rc_T, CB = c->CB;
     const int nbi = (int)((m + 63) / 64), nbs = c->nstripes;
-    // The tie-to-tie walk when its workers fit: at most 4 columns per lane (a worker stages its
-    // block's 3 x 64 x 64*TD entries in LDS) and o <= 14 (X'-H', Y'-H' saturated at o+1 index a 1024-entry LUT).
-    // GA_RC_JUMP=0 keeps the walk of traceback words.
-    {
-        const char* e = c->knob("GA_RC_JUMP");
-        c->rc_jump = (e ? atoi(e) != 0 : kRcJumpDefault) && TD <= 4 && c->o <= 14 &&
-                     ga::rc_jump_lds_bytes(TD, c->rc_every_used) + 12 * 1024 <= 160 * 1024;
-    }
-    if (c->rc_jump)
-        HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * 4 * TD * 6144 + 65536));
-    // (+ one 64-column stripe of slack: a loader reads whole 1 KiB runs)
-    else HIPCHK(c->rc_tb.ensure((size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * TD * 64 * 64 * CB + (size_t)64 * 64 * 4 * 4));
+    c->rc_jump = rc_jump_wanted(c, TD);
+    HIPCHK(c->rc_tb.ensure(rc_cache_bytes(c->rc_jump, TD, CB)));
     const size_t nflags = (size_t)nbi * nbs;
     // the cache slots' owner tags (ga::rc_slot_tag) carry the epoch's ready value: cleared with the flags
     const size_t nown = (size_t)ga::RC_CACHE_I * ga::RC_CACHE_S * sizeof(unsigned long long);
@@ -1391,7 +1172,11 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     if (const char* e = c->knob("GA_RC_TAG_FAULT")) r.tag_fault = std::max(0, atoi(e));
     r.pos = c->rc_pos.as<unsigned>();
     r.tile0 = (int)((((st.i - 1) / 64) << 16) | ((st.j - c->col0 - 1) / 64));  // the walk's first tile
+#ifdef GA_EXPERIMENTS
     r.worker_bytes = c->rc_jump ? ga::rc_jump_worker_bytes_host(TD, r.stck_every) : ga::rc_worker_bytes(TD, CB, r.stck_every);
+#else
+    r.worker_bytes = ga::rc_worker_bytes(TD, CB, r.stck_every);
+#endif
     // one worker per workgroup (one per CU) by default: C3 blocks 14.7 us against 16.5 at three per CU,
     // the walker's tile waits 0.07 against 0.5 ms (tools/exp/r3_rc_diag.py)
     r.workers = c->rc_jump ? 1 : std::max(1, std::min(16, (int)((256 * 256 * 2 - 1024) / r.worker_bytes)));
@@ -1448,8 +1233,11 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     int nserv = 64;
     if (const char* e = c->knob("GA_RC_SERVERS")) nserv = std::max(1, std::min(255, atoi(e)));
     HIPCHK(hipEventRecord(wb.ev0, wb.stream));
+#ifdef GA_EXPERIMENTS
     if (c->rc_jump) ga::launch_walk_rc_jump(wb.stream, w, r, nserv);
-    else ga::launch_walk_rc(wb.stream, w, r, nserv);
+    else
+#endif
+        ga::launch_walk_rc(wb.stream, w, r, nserv);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(wb.ev1, wb.stream));
     return GA_OK;
@@ -1460,6 +1248,7 @@ bool rc_slab_eligible(ga_ctx* c) {
     const char* e = c->knob("GA_RC");
     const int mode = e ? atoi(e) : -1;
     if (mode == 0 || c->qbytes != 1 || c->K > 32 || c->m < 256 || c->n < 256) return false;
+    if (!rc_rows_fit(c->m)) return false;  // the lean checkpoint store's 32-bit buffer (ga_check.h)
     if (mode == 1) return true;
     // C3 (10^10 cells) and up; C5 (20k x 20k protein) kept the stored-words path: its rc lane fill (313
     // stripes at TD = 1 for 20k rows) took 4.8 ms against the row scan's 1.8 (tools/exp/r3 bench_c5 logs)
@@ -2282,17 +2071,51 @@ int ga_device_count(int* count) {
     return GA_OK;
 }
 
-int ga_ctx_create(int device, ga_ctx** out) {
+int ga_ctx_create(int device, ga_ctx** out) { return ga_ctx_create_opts(device, nullptr, out); }
+
+int ga_ctx_create_opts(int device, const char* options, ga_ctx** out) {
     if (!out) return fail(GA_E_ARG, "null out");
+    // the knobs, once (ga_ctx::knobs): the environment's shipped ones, then the options ("NAME=VALUE" entries
+    // separated by ';' or newlines), checked before any device work
+    std::map<std::string, std::string> knobs;
+    for (char** e = environ; e && *e; e++)
+        if (!strncmp(*e, "GA_", 3))
+            if (const char* eq = strchr(*e, '=')) {
+                std::string name(*e, (size_t)(eq - *e));
+                if (env_knob(name)) knobs[name] = eq + 1;
+            }
+    if (options) {
+        std::string s(options), item;
+        for (size_t p = 0; p <= s.size(); p++) {
+            if (p < s.size() && s[p] != ';' && s[p] != '\n') {
+                item += s[p];
+                continue;
+            }
+            if (!item.empty()) {
+                const size_t eq = item.find('=');
+                if (eq == std::string::npos || item.compare(0, 3, "GA_") != 0)
+                    return fail(GA_E_ARG, "bad option '" + item + "' (expected GA_NAME=VALUE)");
+                knobs[item.substr(0, eq)] = item.substr(eq + 1);
+            }
+            item.clear();
+        }
+    }
+    {
+        // GA_RC_EVERY: the checkpoint spacing is a power of two (a mask and a shift per iteration)
+        const auto it = knobs.find("GA_RC_EVERY");
+        if (it != knobs.end()) {
+            const long v = atol(it->second.c_str());
+            if (v < 64 || (v & (v - 1)) != 0 || v > (1L << 20))
+                return fail(GA_E_ARG, "GA_RC_EVERY must be a power of two in [64, 2^20], not '" + it->second + "'");
+        }
+    }
     int n = 0;
     HIPCHK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(GA_E_ARG, "no such HIP device");
     HIPCHK(hipSetDevice(device));
     ga_ctx* c = new ga_ctx();
     c->device = device;
-    for (char** e = environ; e && *e; e++)  // the GA_* overrides, once (ga_ctx::knobs)
-        if (!strncmp(*e, "GA_", 3))
-            if (const char* eq = strchr(*e, '=')) c->knobs[std::string(*e, (size_t)(eq - *e))] = eq + 1;
+    c->knobs = std::move(knobs);
     {
         // hardware queues per priority pool: what the HIP runtime read when it started, i.e. the variable
         // as the process first saw it here (a later change, e.g. a module setting it after HIP started,
@@ -2811,6 +2634,18 @@ int ga_debug_rc(ga_ctx* c, unsigned* out4) {
     if (!c || !out4) return fail(GA_E_ARG, "null argument");
     if (!c->rc_pos.p) return fail(GA_E_STATE, "no recompute walk ran");
     HIPCHK(hipMemcpy(out4, c->rc_pos.p, sizeof(unsigned) * 4, hipMemcpyDeviceToHost));
+    return GA_OK;
+}
+
+// How the library was built: bit 0 set in an experiments build (make EXPERIMENTS=1: the measured-and-dropped paths,
+// e.g. the tie-to-tie walk, and every GA_* variable read from the environment).
+int ga_build_flags(int32_t* flags) {
+    if (!flags) return fail(GA_E_ARG, "null argument");
+#ifdef GA_EXPERIMENTS
+    flags[0] = 1;
+#else
+    flags[0] = 0;
+#endif
     return GA_OK;
 }
 

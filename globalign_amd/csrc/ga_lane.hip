@@ -464,6 +464,15 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         t_start = __builtin_amdgcn_s_memrealtime();
         c_start = __builtin_amdgcn_s_memtime();
     }
+    // DBG: when the wave started the sub-chunks of rows 256, 1024, 4096 and 16384 (how the lag between two stripes
+    // grows along the rows: tools/lane_stamps.py "lag_by_row")
+    unsigned long long t_rows[4] = {0, 0, 0, 0};
+    auto dbg_rows = [&](int r0) {
+        if (r0 == 256) t_rows[0] = __builtin_amdgcn_s_memrealtime();
+        if (r0 == 1024) t_rows[1] = __builtin_amdgcn_s_memrealtime();
+        if (r0 == 4096) t_rows[2] = __builtin_amdgcn_s_memrealtime();
+        if (r0 == 16384) t_rows[3] = __builtin_amdgcn_s_memrealtime();
+    };
     auto wait_ge = [&](unsigned* ctr, unsigned add, unsigned& cached, int target, int kind) {
         unsigned spins = 0;
         cached = sgpr_u(cached);
@@ -483,6 +492,13 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     int4 A[NE], B[NE];
     uint32_t qA[TD][NQ], qB[TD][NQ];
     wait_ge(prod_in, 0, avail, SUB, 0);
+    // DBG: the first wait is the chain's ramp (a stripe's left neighbour has not reached row SUB yet), not a stall
+    // of the steady state
+    unsigned long long w_first = 0, t_first = 0;
+    if (DBG) {
+        w_first = wcyc[0];
+        t_first = __builtin_amdgcn_s_memrealtime();
+    }
     // the edge rows: lane 0 reads them from the ring, lanes 1..63 read the zero block (the asm step adds the
     // edge register to the zero-filled DPP shift; the compiler's step takes lane 0's value only)
     const int4* const ezero = reinterpret_cast<const int4*>(smem + LK_ZERO_OFF);
@@ -810,6 +826,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         auto iteration = [&](int it, auto LEANT) {
             const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
+            if (DBG) dbg_rows(r0);
             if (CB > 0 && SUB == 16) {
                 sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, LEANT);
                 emit(2 * it);
@@ -848,6 +865,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         // their register arrays in scratch)
         for (int it = 0; it < nit; it++) {
             const int r0 = __builtin_amdgcn_readfirstlane(it * 2 * SUB);
+            if (DBG) dbg_rows(r0);
             if (CB > 0 && SUB == 16) {
                 sub_chunk(r0, A, B, qA, qB, std::integral_constant<int, 0>{}, std::false_type{});
                 emit(2 * it);
@@ -885,6 +903,10 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         d[5] = __builtin_amdgcn_s_memtime() - c_start;
         d[6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID: wave, SIMD, CU, SE
         d[7] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID: the XCD (bits 3:0)
+        d[12] = w_first;
+        d[13] = t_first;
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[14 + k] = t_rows[k];
     }
 }
 

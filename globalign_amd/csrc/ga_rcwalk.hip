@@ -22,7 +22,9 @@
 #include "ga_lane.h"
 #include "ga_sync.h"
 #include "ga_walk.h"
+#ifdef GA_EXPERIMENTS  // the tie-to-tie walk: measured slower than the word walk, experiments only
 #include "ga_jump.h"
+#endif
 
 namespace ga {
 
@@ -205,6 +207,10 @@ __device__ bool rc_block(const RcArgs& r, const int8_t* stab, uint8_t* wl, int b
     return true;
 }
 
+constexpr int JLUT_OFF = 2048;                 // (tie-to-tie walk) after the int16 sub' table
+constexpr int JWORK_OFF = JLUT_OFF + 1024 * 16;  // then the workers
+
+#ifdef GA_EXPERIMENTS
 // ---------------------------------------------------------------------------------------------------------------
 // The tie-to-tie walk's workers (ga_jump.h): the same recompute, but instead of traceback codes each
 // cell's three jump entries (one per entering level), built in the same skewed order as the cells themselves: the
@@ -221,8 +227,6 @@ constexpr int JSTAGE_ROWS = 65;  // the block's 64 rows + a scratch row for lane
 __host__ __device__ inline int rc_jump_worker_bytes(int TD, int every) {
     return 3 * JSTAGE_ROWS * 64 * TD * 2 + rc_aw(every) * 4 + rc_aw(every) * 8;
 }
-constexpr int JLUT_OFF = 2048;                 // after the int16 sub' table
-constexpr int JWORK_OFF = JLUT_OFF + 1024 * 16;  // then the workers
 
 template <int TD>
 __device__ bool rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4* lut, uint8_t* wl, int bi, int bs,
@@ -414,6 +418,7 @@ __device__ bool rc_block_jump(const RcArgs& r, const int16_t* stab, const uint4*
         }
     return true;
 }
+#endif  // GA_EXPERIMENTS
 
 template <int TD, int CB, bool JUMP = false>
 __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
@@ -461,8 +466,11 @@ __device__ void rc_server(const RcArgs& r, uint8_t* dyn) {
                 unsigned long long* const own = r.own + rc_slot(bi_i, bs_i);
                 if (lane == 0) __hip_atomic_store(own, 0ull, RLX, AGENT);
                 bool wrote;
+#ifdef GA_EXPERIMENTS
                 if constexpr (JUMP) wrote = rc_block_jump<TD>(r, stab16, lut, wl, bi_i, bs_i, lane);
-                else wrote = rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
+                else
+#endif
+                    wrote = rc_block<TD, CB>(r, stab, wl, bi_i, bs_i, lane);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word written before the tag
                 // (GA_RC_TAG_FAULT: a lost tag, which the walk's loaders must repair through a recompute)
                 const bool fault = r.tag_fault > 0 && ++nblk % (unsigned)r.tag_fault == 0;
@@ -493,6 +501,7 @@ __global__ void __launch_bounds__(64 * WALK_WAVES) walk_rc_kernel(WalkArgs w, Rc
     else rc_server<TD, CB>(r, dyn);
 }
 
+#ifdef GA_EXPERIMENTS
 // the tie-to-tie walk: workgroup 0 walks with jump entries, the others build them
 template <int TD>
 __global__ void __launch_bounds__(64 * JWALK_WAVES) walk_rc_jump_kernel(WalkArgs w, RcArgs r) {
@@ -519,6 +528,7 @@ void launch_walk_rc_jump(hipStream_t s, const WalkArgs& w, const RcArgs& r, int 
         default: launch_rc_jump_one<4>(s, w, r, nserv); break;
     }
 }
+#endif  // GA_EXPERIMENTS
 
 template <int CB, int TD>
 static void launch_rc_one(hipStream_t s, const WalkArgs& w, const RcArgs& r, int nserv) {

@@ -52,9 +52,16 @@ const char* ga_last_error(void);
 /* Number of visible HIP devices. */
 int ga_device_count(int* count);
 
-/* Create / destroy a context on HIP device `device`. */
+/* Create / destroy a context on HIP device `device`.  ga_ctx_create reads the shipped GA_* environment knobs
+ *  once; ga_ctx_create_opts also takes explicit options, "GA_NAME=VALUE" entries separated by ';' or
+ * newlines (kernel variants for tests and tuning, fault injection, diagnostics: never read from the environment).
+ * No reference counterpart: the reference has no device context. */
 int ga_ctx_create(int device, ga_ctx** out);
+int ga_ctx_create_opts(int device, const char* options, ga_ctx** out);
 void ga_ctx_destroy(ga_ctx* ctx);
+
+/* How the library was built: flags[0] bit 0 = an experiments build (measured-and-dropped paths compiled in). */
+int ga_build_flags(int32_t* flags);
 
 /* Load a problem: sequence codes (host), tables, optional custom boundaries.
  * Replaces make_dp_array (globaligner.py:756-821): when row0/col0 are NULL the

@@ -47,6 +47,9 @@ def lib():
                                          C.c_int, i64p, u32p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(I64),
                                          C.POINTER(I64)]
         L.gao_mt_draws.argtypes = [u32p, C.c_int, i32p, i32p]
+        L.gao_align_ckpt.argtypes = [u8p, I64, u8p, I64, C.c_char_p, C.c_char_p, i64p, C.c_int, i64p, i64p, I64, i64p,
+                                     i64p, C.c_int, I64, I64, u32p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(I64),
+                                     C.POINTER(I64), i64p, C.POINTER(I64)]
         _lib = L
     return _lib
 
@@ -111,9 +114,12 @@ def fill_slab(tab, a, b, o, row0, col0):
     return right
 
 
-def align(seq_1, seq_2, cmat, o, mt_words, mode="auto"):
+def align(seq_1, seq_2, cmat, o, mt_words, mode="auto", threads=8, tile=(4096, 4096)):
     """Oracle of make_dp_array + dp_array_forward + dp_array_backward.
 
+    mode "full" (the whole triple array), "sets" (m x n rank sets), "ckpt" (every tile[0]-th row and tile[1]-th
+    column of triples from a forward pass on `threads` threads; the walk recomputes one tile's sets at a time:
+    memory (m/BH)(n+1) + (n/CW)(m+1) triples, for 1M x 1M at 4096 x 4096 12 GB).
     Returns dict(cost, strings, status ('ok'|'IndexError'), ndispatch, mt_out)."""
     tab = Tables(cmat)
     a, b = tab.codes(seq_1), tab.codes(seq_2)
@@ -135,6 +141,13 @@ def align(seq_1, seq_2, cmat, o, mt_words, mode="auto"):
         last = dp[m, n]
         st = lib().gao_traceback_full(dp.reshape(-1), m, n, o, a, b, a_chr, b_chr, tab.sub, tab.K, tab.gh, mt,
                                       oa, om, ob, C.byref(ln), C.byref(nd))
+    elif mode == "ckpt":
+        last = np.zeros(3, np.int64)
+        nt = I64(0)
+        st = lib().gao_align_ckpt(a, m, b, n, a_chr, b_chr, tab.sub, tab.K, tab.gh, tab.gv, o, row0, col0, threads,
+                                  tile[0], tile[1], mt, oa, om, ob, C.byref(ln), C.byref(nd), last, C.byref(nt))
+        if st < 0:
+            raise MemoryError("gao_align_ckpt: checkpoints do not fit in host memory")
     else:
         sets = np.zeros(m * n, np.uint16)
         last = np.zeros(3, np.int64)

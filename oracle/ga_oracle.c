@@ -201,14 +201,18 @@ static void ranks_of(const i64* c, int* rk) {
 
 /* Cell access for the walk.  mode 0: full value array; mode 1: rank sets for
  * interior cells plus boundary triples. */
+struct tiles_s;
 typedef struct {
     int mode;
     i64 m, n, o;
     const i64* dp;        /* mode 0: (m+1)(n+1)x3 */
     const uint16_t* sets; /* mode 1: m x n */
-    const i64* row0;      /* mode 1 */
-    const i64* col0;      /* mode 1 */
+    const i64* row0;      /* mode 1, 2 */
+    const i64* col0;      /* mode 1, 2 */
+    struct tiles_s* tiles; /* mode 2: rank sets of one tile at a time, recomputed from checkpoints (gao_align_ckpt) */
 } cells_t;
+
+static int tile_set(struct tiles_s* t, i64 ri, i64 rj);
 
 /* Ranks of (values + level offsets).  For interior cells in mode 1 the rank
  * tuple is rebuilt from the argmin set: ties among the minima -> rank 0, the
@@ -223,7 +227,7 @@ static void cell_ranks(const cells_t* cs, i64 ri, i64 rj, int level, const i64 a
         ranks_of(c, rk);
         return;
     }
-    int set = (cs->sets[(ri - 1) * cs->n + (rj - 1)] >> (3 * level)) & 7;
+    int set = (cs->mode == 2 ? tile_set(cs->tiles, ri, rj) : cs->sets[(ri - 1) * cs->n + (rj - 1)]) >> (3 * level) & 7;
     /* minima get rank 0, the others distinct ranks starting at the number of
      * minima (what sorted().index yields when the non-minima differ; when they
      * tie the reference key differs but maps to the same move). */
@@ -329,7 +333,7 @@ int gao_traceback(const cells_t* cs, const uint8_t* a, const uint8_t* b, const c
 int gao_traceback_full(const i64* dp, i64 m, i64 n, i64 o, const uint8_t* a, const uint8_t* b,
                        const char* a_chr, const char* b_chr, const i64* sub, int K, const i64* gh,
                        uint32_t* mt_state, char* out_a, char* out_mid, char* out_b, i64* out_len, i64* nd) {
-    cells_t cs = {0, m, n, o, dp, NULL, NULL, NULL};
+    cells_t cs = {0, m, n, o, dp, NULL, NULL, NULL, NULL};
     return gao_traceback(&cs, a, b, a_chr, b_chr, sub, K, gh, 0, mt_state, out_a, out_mid, out_b, out_len, nd);
 }
 
@@ -337,7 +341,7 @@ int gao_traceback_sets(const uint16_t* sets, const i64* row0, const i64* col0, i
                        const uint8_t* a, const uint8_t* b, const char* a_chr, const char* b_chr, const i64* sub,
                        int K, const i64* gh, uint32_t* mt_state, char* out_a, char* out_mid, char* out_b,
                        i64* out_len, i64* nd) {
-    cells_t cs = {1, m, n, o, NULL, sets, row0, col0};
+    cells_t cs = {1, m, n, o, NULL, sets, row0, col0, NULL};
     return gao_traceback(&cs, a, b, a_chr, b_chr, sub, K, gh, 0, mt_state, out_a, out_mid, out_b, out_len, nd);
 }
 
@@ -448,4 +452,147 @@ void gao_fill_score_parallel(const uint8_t* a, i64 m, const uint8_t* b, i64 n, c
     free(args);
     free((void*)p.done);
     free(p.edges);
+}
+
+/* ------------------------------------------- checkpoint-and-recompute traceback */
+/* The same alignment as gao_fill_sets + gao_traceback_sets without m x n rank sets (test infrastructure: pins the
+ * C4 full-traceback alignment, 10^12 cells; the reference's own traceback reads the whole
+ * dp_array, globaligner.py:395-593).  A forward pass on T threads (the column-slab wavefront above) saves every
+ * BH-th row and every CW-th column of triples; the walk then recomputes, one BH x CW tile at a time, the rank sets
+ * of the tile it is in, from the tile's top row and left column (gao_cell, the literal get_next_best_costs), and
+ * reads them exactly as mode 1 does.  The walk only moves up and left, so each tile is recomputed once. */
+typedef struct tiles_s {
+    const uint8_t* a; const uint8_t* b; const i64* sub; int K; const i64* gh; const i64* gv; i64 o;
+    i64 m, n, BH, CW;
+    const i64* row0; const i64* col0;
+    const i64* rowck;   /* [m / BH][n + 1][3]: row k*BH, k >= 1 */
+    const i64* colck;   /* [n / CW][m + 1][3]: column k*CW, k >= 1 */
+    i64 bi, bj;         /* the tile held (-1: none) */
+    uint16_t* sets;     /* [BH][CW] */
+    i64* prev; i64* cur;
+    i64 recomputed;
+} tiles_t;
+
+static int tile_set(tiles_t* t, i64 ri, i64 rj) {
+    const i64 bi = (ri - 1) / t->BH, bj = (rj - 1) / t->CW;
+    if (bi != t->bi || bj != t->bj) {
+        const i64 r0 = bi * t->BH, c0 = bj * t->CW;
+        const i64 r1 = r0 + t->BH < t->m ? r0 + t->BH : t->m, c1 = c0 + t->CW < t->n ? c0 + t->CW : t->n;
+        const i64 w = c1 - c0;
+        const i64* top = bi == 0 ? t->row0 : t->rowck + (size_t)(bi - 1) * 3 * (t->n + 1);
+        const i64* left = bj == 0 ? t->col0 : t->colck + (size_t)(bj - 1) * 3 * (t->m + 1);
+        memcpy(t->prev, &top[3 * c0], sizeof(i64) * 3 * (w + 1));
+        for (i64 i = r0 + 1; i <= r1; i++) {
+            memcpy(t->cur, &left[3 * i], sizeof(i64) * 3);
+            const int ai = t->a[i - 1];
+            for (i64 j = 1; j <= w; j++) {
+                const int bj1 = t->b[c0 + j - 1];
+                gao_cell(&t->prev[3 * (j - 1)], &t->cur[3 * (j - 1)], &t->prev[3 * j], t->sub[ai * t->K + bj1],
+                         t->gh[bj1], t->gv[ai], t->o, &t->cur[3 * j]);
+                t->sets[(i - r0 - 1) * t->CW + (j - 1)] = (uint16_t)cell_sets(&t->cur[3 * j], t->o);
+            }
+            i64* x = t->prev; t->prev = t->cur; t->cur = x;
+        }
+        t->bi = bi;
+        t->bj = bj;
+        t->recomputed++;
+    }
+    return t->sets[(ri - 1 - bi * t->BH) * t->CW + (rj - 1 - bj * t->CW)];
+}
+
+typedef struct {
+    const uint8_t* a; i64 m; const uint8_t* b; i64 n; const i64* sub; int K; const i64* gh; const i64* gv; i64 o;
+    const i64* row0; int T; i64 B, BH, CW;
+    i64* edges; _Atomic i64* done; i64* rowck; i64* colck; i64* last;
+} ckf_t;
+
+typedef struct { ckf_t* p; int k; } ckf_arg;
+
+static void* ckf_worker(void* vp) {
+    ckf_arg* pa = (ckf_arg*)vp;
+    ckf_t* p = pa->p;
+    const int k = pa->k;
+    const i64 c0 = p->n * k / p->T, c1 = p->n * (k + 1) / p->T, w = c1 - c0;
+    i64* prev = (i64*)malloc(sizeof(i64) * 3 * (w + 1));
+    i64* cur = (i64*)malloc(sizeof(i64) * 3 * (w + 1));
+    memcpy(prev, &p->row0[3 * c0], sizeof(i64) * 3 * (w + 1));
+    const i64* left = p->edges + (size_t)k * 3 * (p->m + 1);
+    i64* right = p->edges + (size_t)(k + 1) * 3 * (p->m + 1);
+    memcpy(&right[0], &p->row0[3 * c1], sizeof(i64) * 3);
+    /* the checkpoint columns inside this slab (c0, c1] and their row 0 */
+    const i64 q0 = c0 / p->CW + 1, q1 = c1 / p->CW;
+    for (i64 q = q0; q <= q1; q++) memcpy(&p->colck[(size_t)(q - 1) * 3 * (p->m + 1)], &p->row0[3 * q * p->CW], sizeof(i64) * 3);
+    for (i64 r0 = 1; r0 <= p->m; r0 += p->B) {
+        const i64 r1 = r0 + p->B - 1 < p->m ? r0 + p->B - 1 : p->m;
+        if (k > 0)
+            while (atomic_load_explicit(&p->done[k - 1], memory_order_acquire) < r1) sched_yield();
+        for (i64 i = r0; i <= r1; i++) {
+            memcpy(cur, &left[3 * i], sizeof(i64) * 3);
+            const uint8_t ai = p->a[i - 1];
+            for (i64 j = 1; j <= w; j++)
+                gao_cell(&prev[3 * (j - 1)], &cur[3 * (j - 1)], &prev[3 * j], p->sub[ai * p->K + p->b[c0 + j - 1]],
+                         p->gh[p->b[c0 + j - 1]], p->gv[ai], p->o, &cur[3 * j]);
+            memcpy(&right[3 * i], &cur[3 * w], sizeof(i64) * 3);
+            for (i64 q = q0; q <= q1; q++)
+                memcpy(&p->colck[(size_t)(q - 1) * 3 * (p->m + 1) + 3 * i], &cur[3 * (q * p->CW - c0)], sizeof(i64) * 3);
+            if (i % p->BH == 0 && i / p->BH <= p->m / p->BH)
+                memcpy(&p->rowck[(size_t)(i / p->BH - 1) * 3 * (p->n + 1) + 3 * c0], cur, sizeof(i64) * 3 * (w + 1));
+            i64* t = prev; prev = cur; cur = t;
+        }
+        atomic_store_explicit(&p->done[k], r1, memory_order_release);
+    }
+    if (k == p->T - 1) memcpy(p->last, &prev[3 * w], sizeof(i64) * 3);
+    free(prev);
+    free(cur);
+    return NULL;
+}
+
+/* Returns as gao_traceback (0 ok, 1 IndexError, -1 out of memory); *ntiles: tiles the walk recomputed. */
+int gao_align_ckpt(const uint8_t* a, i64 m, const uint8_t* b, i64 n, const char* a_chr, const char* b_chr,
+                   const i64* sub, int K, const i64* gh, const i64* gv, i64 o, const i64* row0, const i64* col0,
+                   int T, i64 BH, i64 CW, uint32_t* mt_state, char* out_a, char* out_mid, char* out_b, i64* out_len,
+                   i64* nd, i64* last, i64* ntiles) {
+    if (T < 1) T = 1;
+    if (T > n) T = (int)n;
+    if (BH < 1) BH = 1;
+    if (CW < 1) CW = 1;
+    ckf_t p = {a, m, b, n, sub, K, gh, gv, o, row0, T, 256, BH, CW, NULL, NULL, NULL, NULL, last};
+    const i64 nbr = m / BH, nbc = n / CW;
+    p.edges = (i64*)malloc(sizeof(i64) * 3 * (size_t)(m + 1) * (T + 1));
+    p.rowck = (i64*)malloc(sizeof(i64) * 3 * (size_t)(n + 1) * (nbr > 0 ? nbr : 1));
+    p.colck = (i64*)malloc(sizeof(i64) * 3 * (size_t)(m + 1) * (nbc > 0 ? nbc : 1));
+    p.done = (_Atomic i64*)calloc(T, sizeof(i64));
+    tiles_t tl = {a, b, sub, K, gh, gv, o, m, n, BH, CW, row0, col0, NULL, NULL, -1, -1, NULL, NULL, NULL, 0};
+    tl.sets = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)BH * CW);
+    tl.prev = (i64*)malloc(sizeof(i64) * 3 * (CW + 1));
+    tl.cur = (i64*)malloc(sizeof(i64) * 3 * (CW + 1));
+    int status = -1;
+    if (p.edges && p.rowck && p.colck && p.done && tl.sets && tl.prev && tl.cur) {
+        memcpy(p.edges, col0, sizeof(i64) * 3 * (m + 1));
+        pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * T);
+        ckf_arg* args = (ckf_arg*)malloc(sizeof(ckf_arg) * T);
+        for (int k = 0; k < T; k++) {
+            args[k].p = &p;
+            args[k].k = k;
+            pthread_create(&th[k], NULL, ckf_worker, &args[k]);
+        }
+        for (int k = 0; k < T; k++) pthread_join(th[k], NULL);
+        free(th);
+        free(args);
+        free(p.edges);
+        p.edges = NULL;
+        tl.rowck = p.rowck;
+        tl.colck = p.colck;
+        cells_t cs = {2, m, n, o, NULL, NULL, row0, col0, &tl};
+        status = gao_traceback(&cs, a, b, a_chr, b_chr, sub, K, gh, 0, mt_state, out_a, out_mid, out_b, out_len, nd);
+    }
+    *ntiles = tl.recomputed;
+    free(p.edges);
+    free(p.rowck);
+    free(p.colck);
+    free((void*)p.done);
+    free(tl.sets);
+    free(tl.prev);
+    free(tl.cur);
+    return status;
 }

@@ -54,3 +54,16 @@ def _restore_random_state():
     st = random.getstate()
     yield
     random.setstate(st)
+
+
+def set_knob(monkeypatch, name, value):
+    """A GA_* option for engines created from here on, through _native.OPTIONS (ga_ctx_create_opts): the library
+    reads only its shipped knobs from the environment, and none of the test variants or fault injections."""
+    from globalign_amd import _native
+    monkeypatch.setitem(_native.OPTIONS, name, str(value))
+
+
+def del_knob(monkeypatch, name, raising=False):
+    from globalign_amd import _native
+    monkeypatch.delitem(_native.OPTIONS, name, raising=False)
+    monkeypatch.delenv(name, raising=False)

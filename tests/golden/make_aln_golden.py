@@ -2,6 +2,8 @@
 
     python tests/golden/make_aln_golden.py c3   ->  tests/golden/c3_aln.json   (10^10 cells, ~20 GB of sets)
     python tests/golden/make_aln_golden.py c5   ->  tests/golden/c5_aln.json
+    python tests/golden/make_aln_golden.py c4tb ->  tests/golden/c4tb_aln.json (10^12 cells: the checkpoint-and-
+        recompute walk gao_align_ckpt on 8 threads, 12 GB of row / column checkpoints, ~20 min here)
 
 The walk runs under random.seed(0) exactly as bench.py / the GPU test do; the record holds the
 alignment length, the sha256 digests of the three strings (tests/conftest.py aln_digest) and of the
@@ -29,14 +31,20 @@ def aln_record(name):
                                                blosum=load_matrix(mat) if mat else None)
     random.seed(0)
     t0 = time.time()
-    r = core.align(s1, s2, cmat, goc, core.mt_state_array(), mode="sets")
+    # 10^12 cells (C4 with full traceback): no m x n sets; the checkpoint-and-recompute walk, which reproduces the
+    # sets walk's C3 alignment and random state exactly (tests/test_oracle.py runs it on every reference-run case)
+    ckpt = wl["m"] * wl["n"] > 10**11
+    mode = "ckpt" if ckpt else "sets"
+    r = core.align(s1, s2, cmat, goc, core.mt_state_array(), mode=mode, threads=int(os.environ.get("ORACLE_THREADS", 8)))
     a, mid, b = r["strings"]
     st = random.getstate()
     after = (st[0], tuple(int(x) for x in r["mt_out"]), st[2])
     return {"workload": wl["desc"], "m": wl["m"], "n": wl["n"], "seed": 0, "cost": r["cost"],
             "status": r["status"], "ndispatch": r["ndispatch"], "aln_len": len(mid),
             "aln_sha16": aln_digest(a, mid, b), "state_sha32": state_digest(after),
-            "oracle": "oracle/ga_oracle.c gao_fill_sets + gao_traceback_sets", "seconds": round(time.time() - t0, 1)}
+            "oracle": "oracle/ga_oracle.c " + ("gao_align_ckpt (4096 x 4096 tiles)" if ckpt else
+                                               "gao_fill_sets + gao_traceback_sets"),
+            "seconds": round(time.time() - t0, 1)}
 
 
 if __name__ == "__main__":

@@ -14,7 +14,7 @@ import socket
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob, del_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -27,6 +27,11 @@ def _free_port():
     return port
 
 
+def _parent_options():
+    from globalign_amd import _native
+    return dict(_native.OPTIONS)
+
+
 def _scoring(seq_1, seq_2):
     from globalign_amd.scoring import validate_and_transform_args
     _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, seq_1[:64], seq_2[:64], match_score=2,
@@ -36,11 +41,12 @@ def _scoring(seq_1, seq_2):
 
 
 def _worker(rank, world, port, seq_1, seq_2, mt_words, band, out_path, traceback=True, fail_import=False,
-            fail_export=False):
+            fail_export=False, options=None):
     import torch
     import torch.distributed as dist
-    from globalign_amd import distributed
+    from globalign_amd import _native, distributed
     from globalign_amd._native import CostTables
+    _native.OPTIONS.update(options or {})  # the parent's context options (a spawned rank starts without them)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -92,8 +98,8 @@ def _slabs_match_oracle(world, m, n, seed, band, tmp_path):
     random.seed(seed)
     mt_words = np.array(random.getstate()[1], dtype=np.uint32)
     out = str(tmp_path / "res.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out, True, False, False,
+                                      _parent_options()), nprocs=world, join=True, start_method="spawn")
     r = np.load(out)
     cmat, goc = _scoring(seq_1, seq_2)
     ref = core.align(seq_1, seq_2, cmat, goc, mt_words)
@@ -120,8 +126,8 @@ def _slabs_score_only_match_oracle(world, m, n, seed, band, tmp_path):
     random.seed(seed)
     mt_words = np.array(random.getstate()[1], dtype=np.uint32)
     out = str(tmp_path / "res_so.npz")
-    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out, False), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), seq_1, seq_2, mt_words, band, out, False, False, False,
+                                      _parent_options()), nprocs=world, join=True, start_method="spawn")
     r = np.load(out)
     cmat, goc = _scoring(seq_1, seq_2)
     tab = core.Tables(cmat)
@@ -136,8 +142,8 @@ def test_gpu_slabs_score_only_diag_match_oracle(td, monkeypatch, tmp_path):
     """The anti-diagonal fill (GA_FILL_MODE=diag; no longer chosen automatically) in slab mode:
     the left edge from the neighbour rank's progress word, the right edge out to it, the cost from the last
     rank."""
-    monkeypatch.setenv("GA_FILL_MODE", "diag")
-    monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
+    set_knob(monkeypatch, "GA_FILL_MODE", "diag")
+    set_knob(monkeypatch, "GA_DIAG_COLS_PER_LANE", str(td))
     _slabs_score_only_match_oracle(2, 4000, 30_000 + 77, 45 + td, 1024, tmp_path)
     _slabs_score_only_match_oracle(3, 12_000, 2_000 + 5, 47 + td, 2048, tmp_path)
 
@@ -173,13 +179,13 @@ def test_gpu_slabs_recompute_walk_match_oracle(world, m, n, seed, band, tmp_path
     fill stores checkpoints only (no m x n words, so C4 traceback fits at N = 2 / 4), and each slab walk,
     handed on right to left, recomputes the blocks ahead of it -- the leftmost slabs' stripe 0 from the
     halo the left neighbour sent."""
-    monkeypatch.setenv("GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC", "1")
     _slabs_match_oracle(world, m, n, seed, band, tmp_path)
 
 
 def test_global_aligner_devices_recompute_walk(monkeypatch):
     """GlobalAligner(devices=[0, 0]) with the recompute walk on each slab."""
-    monkeypatch.setenv("GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC", "1")
     test_global_aligner_devices_in_process([0, 0], 2600, 4200, 53, dict(match_score=2, mismatch_score=-3,
                                                                         gap_open_score=-5, gap_extension_score=-1))
 
@@ -201,9 +207,9 @@ def test_linked_slabs_abort_propagates(monkeypatch):
     a, b = tables.codes(s1), tables.codes(s2)
     # GA_* knobs are read when a context is created: only the middle slab's context gets the short halo bound
     engines = [distributed.GpuSlabEngine(0)]
-    monkeypatch.setenv("GA_HALO_SPIN_LIMIT", str(1 << 16))
+    set_knob(monkeypatch, "GA_HALO_SPIN_LIMIT", str(1 << 16))
     engines.append(distributed.GpuSlabEngine(0))
-    monkeypatch.delenv("GA_HALO_SPIN_LIMIT")
+    del_knob(monkeypatch, "GA_HALO_SPIN_LIMIT")
     engines.append(distributed.GpuSlabEngine(0))
     try:
         edges = distributed.slab_bounds(n, 3)

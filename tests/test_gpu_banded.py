@@ -8,7 +8,7 @@ import random
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob, del_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -25,7 +25,7 @@ def _align(monkeypatch, s1, s2, kw, seed, band_rows, protein=False):
     ref = core.align(a1, a2, cmat, goc, mt)
     _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
     tables = _native.CostTables(cmat2, goc2)
-    monkeypatch.setenv("GA_TB_BAND_ROWS", str(band_rows))
+    set_knob(monkeypatch, "GA_TB_BAND_ROWS", str(band_rows))
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -93,9 +93,9 @@ def test_banded_matches_unbanded_100k(monkeypatch):
     out = []
     for rows in (None, 8192):
         if rows is None:
-            monkeypatch.delenv("GA_TB_BAND_ROWS", raising=False)
+            del_knob(monkeypatch, "GA_TB_BAND_ROWS", raising=False)
         else:
-            monkeypatch.setenv("GA_TB_BAND_ROWS", str(rows))
+            set_knob(monkeypatch, "GA_TB_BAND_ROWS", str(rows))
         eng = _native.Engine(0)
         try:
             eng.load(tables.codes(s1), tables.codes(s2), tables)

@@ -8,7 +8,7 @@ import random
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -24,7 +24,7 @@ def _tables(seq_1, seq_2, scoring=SCORING):
 
 def _engine(monkeypatch, T):
     from globalign_amd import _native
-    monkeypatch.setenv("GA_COLS_PER_LANE", str(T))
+    set_knob(monkeypatch, "GA_COLS_PER_LANE", str(T))
     return _native.Engine(0)
 
 

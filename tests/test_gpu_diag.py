@@ -6,7 +6,7 @@ rows shorter than the stripe skew, an int16 profile and host-supplied boundary t
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob, del_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -15,8 +15,8 @@ SCORING = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extensio
 
 def _engine(monkeypatch, td):
     from globalign_amd import _native
-    monkeypatch.setenv("GA_FILL_MODE", "diag")
-    monkeypatch.setenv("GA_DIAG_COLS_PER_LANE", str(td))
+    set_knob(monkeypatch, "GA_FILL_MODE", "diag")
+    set_knob(monkeypatch, "GA_DIAG_COLS_PER_LANE", str(td))
     return _native.Engine(0)
 
 
@@ -81,8 +81,8 @@ def test_auto_tall_score_vs_oracle(monkeypatch, m, n):
     from globalign_amd import _native
     from globalign_amd._native import CostTables
     from globalign_amd.scoring import validate_and_transform_args
-    monkeypatch.delenv("GA_FILL_MODE", raising=False)
-    monkeypatch.delenv("GA_DIAG_COLS_PER_LANE", raising=False)
+    del_knob(monkeypatch, "GA_FILL_MODE", raising=False)
+    del_knob(monkeypatch, "GA_DIAG_COLS_PER_LANE", raising=False)
     s1, s2 = splitmix_seq(m, m + 3, "dna"), splitmix_seq(n, n + 5, "dna")
     _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **SCORING)
     tables = CostTables(cmat, goc)

@@ -7,7 +7,7 @@ host-supplied boundary triples and the finite `big` sentinel of very unequal len
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -28,9 +28,9 @@ def _fill(monkeypatch, td, nwc, s1, s2, kw, **load_kw):
     from globalign_amd import _native
     from globalign_amd._native import CostTables
     from globalign_amd.scoring import validate_and_transform_args
-    monkeypatch.setenv("GA_FILL_MODE", "lane")
-    monkeypatch.setenv("GA_LANE_COLS_PER_LANE", str(td))
-    monkeypatch.setenv("GA_FILL_NWC", str(nwc))
+    set_knob(monkeypatch, "GA_FILL_MODE", "lane")
+    set_knob(monkeypatch, "GA_LANE_COLS_PER_LANE", str(td))
+    set_knob(monkeypatch, "GA_FILL_NWC", str(nwc))
     _, _, _, cmat, _, goc, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
     tables = CostTables(cmat, goc)
     eng = _native.Engine(0)
@@ -118,13 +118,13 @@ def _align_lane(monkeypatch, s1, s2, kw, seed, td, nwc=4, protein=False, band_ro
     ref = core.align(a1, a2, cmat, goc, mt)
     _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
     tables = _native.CostTables(cmat2, goc2)
-    monkeypatch.setenv("GA_FILL_MODE", "lane")
-    monkeypatch.setenv("GA_LANE_COLS_PER_LANE", str(td))
-    monkeypatch.setenv("GA_FILL_NWC", str(nwc))
+    set_knob(monkeypatch, "GA_FILL_MODE", "lane")
+    set_knob(monkeypatch, "GA_LANE_COLS_PER_LANE", str(td))
+    set_knob(monkeypatch, "GA_FILL_NWC", str(nwc))
     if band_rows:
-        monkeypatch.setenv("GA_TB_BAND_ROWS", str(band_rows))
+        set_knob(monkeypatch, "GA_TB_BAND_ROWS", str(band_rows))
     if tb_sub:
-        monkeypatch.setenv("GA_LANE_TB_SUB", str(tb_sub))
+        set_knob(monkeypatch, "GA_LANE_TB_SUB", str(tb_sub))
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -190,7 +190,7 @@ def test_lane_handover_variants(monkeypatch, env, td):
     the lean asm sub-chunk (default), the IO wave's workgroup hand-off and the last compute wave's direct one
     (GA_LANE_DIRECT=1), the compiler's step (GA_LANE_ASM=0), early edge reads (GA_LANE_LATE=0)."""
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        set_knob(monkeypatch, k, v)
     m, n = 2100, 64 * td * 4 * 12 + 37
     s1, s2 = splitmix_seq(m, 301 + td, "dna"), splitmix_seq(n, 302 + td, "dna")
     got, cmat, goc = _fill(monkeypatch, td, 4, s1, s2, SCORING)

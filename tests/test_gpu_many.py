@@ -11,7 +11,7 @@ import random
 import numpy as np
 import pytest
 
-from tests.conftest import GOLDEN, aln_digest, load_matrix, splitmix_seq, state_digest
+from tests.conftest import GOLDEN, aln_digest, load_matrix, splitmix_seq, state_digest, set_knob
 
 pytestmark = pytest.mark.gpu
 
@@ -96,8 +96,8 @@ def test_align_repeated_pipe_modes(monkeypatch, mode, fills, m, n, seed, count, 
     """The pipeline's fill kernels (GA_PIPE_MODE: lane-skewed narrow fills / row-scan fills) and fills in
     flight give the chained oracle's strings, costs and final random state."""
     import globalign_amd
-    monkeypatch.setenv("GA_PIPE_MODE", mode)
-    monkeypatch.setenv("GA_PIPE_FILLS", fills)
+    set_knob(monkeypatch, "GA_PIPE_MODE", mode)
+    set_knob(monkeypatch, "GA_PIPE_FILLS", fills)
     alpha = "protein" if "scoring_mat_name" in kw else "dna"
     s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
     ref = _chain_oracle(s1, s2, kw, seed, count)
@@ -120,7 +120,7 @@ def test_align_repeated_walk_chain(monkeypatch, chain, m, n, seed, count, kw):
     more alignments than slots (every slot reused), short walks that outrun the tie-break producer, a tall
     pair; each alignment's strings and cost and the final random state equal the chained oracle's."""
     import globalign_amd
-    monkeypatch.setenv("GA_PIPE_CHAIN", chain)
+    set_knob(monkeypatch, "GA_PIPE_CHAIN", chain)
     alpha = "protein" if "scoring_mat_name" in kw else "dna"
     s1, s2 = splitmix_seq(m, seed, alpha), splitmix_seq(n, seed + 1, alpha)
     ref = _chain_oracle(s1, s2, kw, seed, count)

@@ -273,16 +273,18 @@ def test_tall_narrow_vs_oracle(ga):
 
 
 # ---------------------------------------------------------------- bench workloads vs the oracle's cost goldens
-@pytest.mark.parametrize("name", ["c2", "c5", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c2", "c5", "c3", "c4", "c4tb"])
 def test_bench_workload_cost_matches_golden(ga, name):
     """Each bench.py workload at its full BASELINE size (C4 = 10^12 cells, score only) against the cost
     the threaded C oracle produced (tests/golden/make_cost_golden.py, make_c4_golden.py); traceback
     workloads also walk, must reproduce both inputs, and must equal the oracle's alignment strings and
-    final random state (tests/golden/make_aln_golden.py: <name>_aln.json digests, random.seed(0))."""
+    final random state (tests/golden/make_aln_golden.py: <name>_aln.json digests, random.seed(0)).  c4tb: C4 with
+    full traceback on one GPU (the recompute walk), its 1,222,001-column alignment pinned by the oracle's
+    checkpoint-and-recompute walk (gao_align_ckpt)."""
     import bench
     from globalign_amd import _native
     wl = bench.WORKLOADS[name]
-    gold = json.load(open(os.path.join(GOLDEN, f"{name}_cost.json")))["cost"]
+    gold = json.load(open(os.path.join(GOLDEN, f"{wl.get('golden', name)}_cost.json")))["cost"]
     s1, s2 = bench.workload_pair(wl)
     tables, _ = bench.problem_tables(s1, s2, wl["scoring"])
     eng = _native.Engine(0)
@@ -318,3 +320,40 @@ def test_similar_pairs_vs_oracle(ga, monkeypatch, div, lens):
     monkeypatch.setattr(random, "seed", orig)
     _oracle_case(ga, s1, s2, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1),
                  seed=int(div * 100) + 1)
+
+
+# ---------------------------------------------------------------- the walker's lane select
+@pytest.mark.parametrize("n", [5000, 40_000])
+def test_walk_long_diagonal_runs_index_carries(ga, n):
+    """The walker advances its v_readlane lane select unmasked: the index's low byte is the window offset and its
+    upper bytes carry every move's advance (0x080109 >> 8L, ga_walk.h), which the lane select ignores (only its low
+    6 bits count; tools/micro/readlane_idx2.hip).  A pure-diagonal path -- identical sequences, no tie anywhere, every
+    move 0x080109 -- sets those upper bytes on every readlane of the walk: the alignment must be n matches and the
+    random state the one n dispatches (18 draws each, globaligner.py:595-685) leave.  5000: the stored-words walk;
+    40 000: the recompute walk."""
+    s = _fast_splitmix(n, 77)
+    kw = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
+    random.seed(9)
+    r = ga.GlobalAligner(max_seq_len_prod=None, **kw).align(s, s)
+    after = random.getstate()
+    assert r.cost == 0 and r.score == 2 * n
+    assert r.middle_part == "|" * n and r.seq_1_aligned == s and r.seq_2_aligned == s
+    random.seed(9)
+    sizes = (3, 2, 2, 2, 3, 2, 2, 2, 3) * 2
+    for _ in range(n):
+        for k in sizes:
+            random.choice(range(k))
+    assert after == random.getstate()
+
+
+@pytest.mark.parametrize("every,ins", [(97, False), (53, True)])
+def test_walk_diagonal_runs_with_gaps_vs_oracle(ga, every, ins):
+    """Long diagonal runs broken by single gaps (every 97th residue deleted / a residue inserted every 53rd): the
+    index advances of up (0x08) and left (0x0801) moves between diagonal runs, against the oracle."""
+    s1 = _fast_splitmix(6000, 78)
+    if ins:
+        s2 = "".join(c + ("G" if k % every == every - 1 else "") for k, c in enumerate(s1))
+    else:
+        s2 = "".join(c for k, c in enumerate(s1) if k % every != every - 1)
+    _oracle_case(ga, s1, s2, dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1),
+                 seed=every)

@@ -10,12 +10,23 @@ import random
 import numpy as np
 import pytest
 
-from tests.conftest import splitmix_seq
+from tests.conftest import splitmix_seq, set_knob
 
 pytestmark = pytest.mark.gpu
 
 DNA = dict(match_score=2, mismatch_score=-3, gap_open_score=-5, gap_extension_score=-1)
 JUMP_DEFAULT = "0"  # ga_host.cpp kRcJumpDefault
+
+
+def _experiments():
+    from globalign_amd import _native
+    return _native.experiments_build()
+
+
+# the tie-to-tie walk measured slower than the word walk and is compiled only into an experiments
+# build (make EXPERIMENTS=1); its cases run there
+needs_jump = pytest.mark.skipif("not __import__('globalign_amd._native', fromlist=['x']).experiments_build()",
+                                reason="the tie-to-tie walk is in experiments builds only")
 
 
 def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
@@ -30,9 +41,9 @@ def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
     ref = core.align(a1, a2, cmat, goc, mt)
     _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **kw)
     tables = _native.CostTables(cmat2, goc2)
-    monkeypatch.setenv("GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC", "1")
     for k, v in (env or {}).items():
-        monkeypatch.setenv(k, str(v))
+        set_knob(monkeypatch, k, str(v))
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -43,7 +54,8 @@ def _align(monkeypatch, s1, s2, kw, seed, env=None, protein=False):
         eng.close()
     assert kind[0] == "rc", kind  # the recompute path really ran
     # the tie-to-tie walk (jump entries) wherever its workers fit: <= 4 columns per lane, o <= 14
-    jump_ok = kind[1] <= 4 and goc <= 14 and str((env or {}).get("GA_RC_JUMP", os.environ.get("GA_RC_JUMP", JUMP_DEFAULT))) != "0"
+    jump_ok = (_experiments() and kind[1] <= 4 and goc <= 14 and
+               str((env or {}).get("GA_RC_JUMP", os.environ.get("GA_RC_JUMP", JUMP_DEFAULT))) != "0")
     assert walk == ("jump" if jump_ok else "rc"), (walk, kind, goc)
     assert status == 0
     assert int(cost) == ref["cost"]
@@ -91,7 +103,7 @@ def test_rc_worker_pools_vs_oracle(monkeypatch, env):
     assert kind[1] == 4, kind
 
 
-@pytest.mark.parametrize("jump", [0, 1])
+@pytest.mark.parametrize("jump", [0, pytest.param(1, marks=needs_jump)])
 def test_rc_lost_slot_tags_repaired_vs_oracle(monkeypatch, jump):
     """Cache slot owner tags (ga::rc_slot_tag, ADVICE r4): every 3rd block a worker writes is left without its tag,
     as if another block's worker had overwritten the slot; the walk's loaders must never use such a slot, reset the
@@ -136,7 +148,7 @@ def test_rc_repeated_calls_reuse_buffers(monkeypatch):
     from globalign_amd import _native
     from globalign_amd.scoring import validate_and_transform_args
     from oracle import core, transform
-    monkeypatch.setenv("GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC", "1")
     eng = _native.Engine(0)
     try:
         for k, (m, n) in enumerate([(2000, 2100), (900, 3000), (2000, 2100), (3100, 1200)]):
@@ -196,8 +208,8 @@ def test_rc_checkpoints_over_budget_fall_back(monkeypatch):
     ref = core.align(a1, a2, cmat, goc, mt)
     _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **DNA)
     tables = _native.CostTables(cmat2, goc2)
-    monkeypatch.setenv("GA_RC", "1")
-    monkeypatch.setenv("GA_RC_BUDGET_MB", "0")
+    set_knob(monkeypatch, "GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC_BUDGET_MB", "0")
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -223,9 +235,9 @@ def _align_fallback(monkeypatch, env, seed):
     ref = core.align(a1, a2, cmat, goc, mt)
     _, _, _, cmat2, _, goc2, _ = validate_and_transform_args(None, None, s1[:64], s2[:64], **DNA)
     tables = _native.CostTables(cmat2, goc2)
-    monkeypatch.setenv("GA_RC", "1")
+    set_knob(monkeypatch, "GA_RC", "1")
     for k, v in env.items():
-        monkeypatch.setenv(k, str(v))
+        set_knob(monkeypatch, k, str(v))
     eng = _native.Engine(0)
     try:
         eng.load(tables.codes(a1), tables.codes(a2), tables)
@@ -251,7 +263,7 @@ def test_small_device_memory_bands(monkeypatch):
     _align_fallback(monkeypatch, {"GA_DEV_AVAIL_MB": 1}, seed=2)
 
 
-@pytest.mark.parametrize("jump", [0, 1])
+@pytest.mark.parametrize("jump", [0, pytest.param(1, marks=needs_jump)])
 @pytest.mark.parametrize("m,n,seed", [(3000, 2600, 71), (2049, 4100, 72)])
 def test_rc_jump_and_word_walks_vs_oracle(monkeypatch, jump, m, n, seed):
     """Both recompute walks on the same problems: the tie-to-tie walk (jump entries) and the walk of
@@ -260,6 +272,7 @@ def test_rc_jump_and_word_walks_vs_oracle(monkeypatch, jump, m, n, seed):
            env={"GA_RC_JUMP": jump})
 
 
+@needs_jump
 @pytest.mark.parametrize("o", [1, 2, 6, 14])
 def test_rc_jump_gap_opens_vs_oracle(monkeypatch, o):
     """Gap opens across the jump LUT's range (X'-H', Y'-H' saturated at o+1 <= 15), incl. o = 1 and the largest, 14."""

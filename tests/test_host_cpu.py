@@ -7,7 +7,7 @@ import re
 import numpy as np
 import pytest
 
-from tests.conftest import ROOT, state_digest
+from tests.conftest import ROOT, state_digest, set_knob
 
 
 @pytest.fixture(scope="module")
@@ -115,7 +115,7 @@ def test_engine_cache_keeps_one_knob_set(monkeypatch):
     monkeypatch.setattr(_native, "_default", {})
     monkeypatch.setattr(distributed, "_device_engines", {})
     for k in range(5):
-        monkeypatch.setenv("GA_RC_SERVERS", str(48 + k))
+        set_knob(monkeypatch, "GA_RC_SERVERS", str(48 + k))
         e0 = _native.default_engine(0)
         assert _native.default_engine(0) is e0          # same knobs: the cached context
         _native.default_engine(1)

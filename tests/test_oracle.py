@@ -31,11 +31,11 @@ def _smat_for(rec):
     return None, None
 
 
-def _run_oracle(rec, mode="auto"):
+def _run_oracle(rec, mode="auto", **kw):
     blosum, mtx = _smat_for(rec)
     s1, s2, smat, cmat, gos, goc = transform.settings(rec["kwargs"], blosum=blosum, mtx=mtx)
     random.seed(rec["seed"])
-    res = core.align(s1, s2, cmat, goc, core.mt_state_array(), mode=mode)
+    res = core.align(s1, s2, cmat, goc, core.mt_state_array(), mode=mode, **kw)
     res["score"] = transform.cost_to_score(res["cost"], len(s1), len(s2), transform.max_val(smat))
     res["smat"], res["cmat"], res["gos"], res["goc"] = smat, cmat, gos, goc
     return res
@@ -91,19 +91,24 @@ def test_oracle_random_fill():
         _check_fill(rec)
 
 
-@pytest.mark.parametrize("mode", ["full", "sets"])
+@pytest.mark.parametrize("mode", ["full", "sets", "ckpt"])
 def test_oracle_random_api(mode):
+    """Every reference-run API case through each walk of the oracle; "ckpt" (the checkpoint-and-recompute walk that
+    pins the C4 full-traceback alignment, gao_align_ckpt) with tiny tiles and three threads, so that walks cross many
+    tiles and the forward pass many slab boundaries."""
     cases = json.load(open(os.path.join(GOLDEN, "random_api.json")))
     n_err = 0
+    kw = dict(threads=3, tile=(3, 5)) if mode == "ckpt" else {}
     for rec in cases:
         if "error" in rec and rec["error"] != "IndexError":
             continue  # validation errors are host-side, checked in test_api.py
         n_err += "error" in rec
-        _check(rec, _run_oracle(rec, mode=mode))
+        _check(rec, _run_oracle(rec, mode=mode, **kw))
     assert n_err >= 3  # the degenerate IndexError quirk is exercised
 
 
-def test_oracle_splitmix():
+@pytest.mark.parametrize("mode,okw", [("sets", {}), ("ckpt", dict(threads=4, tile=(61, 97))), ("ckpt", dict(threads=1, tile=(1000, 7)))])
+def test_oracle_splitmix(mode, okw):
     for rec in json.load(open(os.path.join(GOLDEN, "splitmix.json"))):
         if rec["m"] * rec["n"] > 5_000_000:
             continue  # 10k x 10k is pinned in the GPU suite (needs ~2 GB of traceback sets)
@@ -112,7 +117,7 @@ def test_oracle_splitmix():
         s2 = splitmix_seq(rec["n"], rec["seeds"][1], rec["alphabet"])
         kw = dict(rec["kwargs"], seq_1=s1, seq_2=s2)
         r = dict(rec, kwargs=kw)
-        res = _run_oracle(r, mode="sets")
+        res = _run_oracle(r, mode=mode, **okw)
         a, mid, b = res["strings"]
         assert res["cost"] == rec["cost"] and res["score"] == rec["score"]
         assert len(mid) == rec["aln_len"]

@@ -5,7 +5,9 @@
 Prints one JSON line: the fill time, the chain's start lags (intra- and cross-workgroup), stripe
 durations, and the cycles each stripe waited for its left edge / the profile / ring space, grouped by
 the SIMD the wave ran on (HW_ID bits 5:4) -- a chain runs at its slowest stripe's pace, and that
-stripe is the one that never waits for its left neighbour."""
+stripe is the one that never waits for its left neighbour.  Every stripe is resident from the kernel's start, so its
+edge wait includes the ramp (stripe s first waits about s lags for its left neighbour to reach row SUB):
+"steady_state" splits that first wait off.""" 
 import ctypes as C
 import json
 import os
@@ -28,6 +30,10 @@ if wl:
 else:
     s1, s2 = bench.splitmix(m, 1), bench.splitmix(n, 2)
     tables, _ = bench.problem_tables(s1, s2)
+# context options for experiments (GA_OPTIONS="GA_NAME=VALUE;..."; the library reads only its shipped knobs from
+# the environment)
+for kv in filter(None, os.environ.get("GA_OPTIONS", "").split(";")):
+    _native.OPTIONS[kv.partition("=")[0]] = kv.partition("=")[2]
 eng = _native.Engine(0)
 eng.load(tables.codes(s1), tables.codes(s2), tables)
 L = _native.load_library()
@@ -37,7 +43,7 @@ plain_ms = eng.kernel_ms()[0]
 L.ga_debug_stamps(eng._h, 1, None, 0)
 cost, _ = eng.fill(traceback=False)
 kind, T, ns, nwc, nslabs = eng.fill_kind()
-W = 12  # LK_DBG_WORDS (ga_lane.h)
+W = 18  # LK_DBG_WORDS (ga_lane.h)
 buf = np.zeros(W * ns, dtype=np.uint64)
 L.ga_debug_stamps(eng._h, 0, buf.ctypes.data, buf.size)
 L.ga_debug_stamps(eng._h, 0, None, 0)
@@ -63,6 +69,34 @@ for sd in range(4):
                             "wait_space_frac": float(np.median(st[sel, 4] / tot[sel])),
                             "cyc_per_step_busy": float(np.median((tot[sel] - st[sel, 2] - st[sel, 3] - st[sel, 4]) /
                                                                  (m + 63)))}
+# the first edge wait (word 12) is the ramp: stripe s waits for its left neighbour to reach row SUB, about s lags after
+# the kernel's start; everything after it (words 2 - 12) is the steady state's waiting
+first_w = st[:, 12]
+steady_w = st[:, 2] - first_w
+t_first = (st[:, 13] - t0) / 100.0
+steady_ns = (end - t_first) * 1e3 / (m + 63)
+dec = np.array_split(np.arange(ns), 10)
+steady = {"wait_edge_first_frac_median": float(np.median(first_w / tot)),
+          "wait_edge_steady_frac_median": float(np.median(steady_w / tot)),
+          "wait_edge_steady_frac_p90": float(np.percentile(steady_w / tot, 90)),
+          "wait_edge_steady_frac_by_decile": [float(np.median(steady_w[d] / tot[d])) for d in dec],
+          "first_edge_us_by_decile": [float(np.median(t_first[d])) for d in dec],
+          "ns_per_step_after_first_edge_median": float(np.median(steady_ns)),
+          "ns_per_step_after_first_edge_by_decile": [float(np.median(steady_ns[d])) for d in dec],
+          "cyc_per_step_after_first_edge_median": float(np.median((tot - first_w) / (m + 63)))}
+# the lag between consecutive stripes at rows 256 / 1024 / 4096 / 16384 (words 14..17), intra- and cross-workgroup
+# links apart: a link's lag is set where it first grows (a consumer never catches up), DESIGN.md 5.6.2
+lag_by_row = {}
+for k, row in enumerate((256, 1024, 4096, 16384)):
+    tr = st[:, 14 + k]
+    if row < m and (tr > 0).all():
+        lr = np.diff((tr - t0) / 100.0)
+        lag_by_row[str(row)] = {"intra_median_us": float(np.median(lr[~cross])) if (~cross).any() else None,
+                                "cross_median_us": float(np.median(lr[cross])) if cross.any() else None,
+                                "cross_p90_us": float(np.percentile(lr[cross], 90)) if cross.any() else None}
+lag_by_row["end"] = {"intra_median_us": float(np.median(elag[~cross])) if (~cross).any() else None,
+                     "cross_median_us": float(np.median(elag[cross])) if cross.any() else None,
+                     "cross_p90_us": float(np.percentile(elag[cross], 90)) if cross.any() else None}
 by_wave = {int(w): {"wait_edge_frac": float(np.median(st[wave_in_wg == w, 2] / tot[wave_in_wg == w])),
                     "simd_mode": int(np.bincount(simd[wave_in_wg == w]).argmax())} for w in range(min(nwc, ns))}
 if os.environ.get("LANE_STAMPS_DUMP"):
@@ -113,5 +147,5 @@ print(json.dumps({
     "stripe_dur_us_median": float(np.median(dur)), "stripe_dur_us_max": float(dur.max()),
     "ns_per_step_median": float(np.median(dur) * 1e3 / (m + 63)),
     "cycles_per_step_median": float(np.median(tot / (m + 63))),
-    "by_simd": by_simd, "by_wave": by_wave, "lag_distribution": dist,
+    "by_simd": by_simd, "by_wave": by_wave, "lag_distribution": dist, "steady_state": steady, "lag_by_row": lag_by_row,
 }), flush=True)
