@@ -70,6 +70,10 @@ struct FillArgs {
     // sub' bytes of rows r .. r+3 of one column code, rows outside 1..m zero), copied into the LDS ring by the profile
     // wave; nullptr: the profile wave computes it from a and sub'
     const uint32_t* qprof;
+    // lane fill, score only: the lean sub-chunk from the first step (ga_lane.hip), allowed when row 0 is uniform in the
+    // shifted domain (H'(0, j) = o and h2'(0, j) = 2o for every column: the reference's boundary with 2o + GH(n) <=
+    // big): lanes still above row 1 then step on zero profile bytes and keep exactly those values
+    int lean0;
 };
 
 // Traceback word layout (fill -> walk): per stripe s, lane l (column 64s+l+1),

@@ -125,6 +125,8 @@ struct ga_ctx {
     int64_t m = 0, n = 0;      // local problem (slab: n = local columns)
     int64_t n_global = 0, col0 = 0;
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
+    int64_t gh_total = 0;      // GH(n_global): the sum of the horizontal gap costs of seq_2
+    int rng_threads = 1;       // host threads building a call's tie-break table (ga_rng.h build_rng_threaded)
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
     int T = 1, T_req = 0, nwc_req = 0;
     int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal, 3 lane-skewed (GA_FILL_MODE)
@@ -355,6 +357,8 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     c->o = o;
     c->big = (int)big;
     c->custom = row0 != nullptr || col0 != nullptr;
+    c->gh_total = 0;  // GH(n) of the whole problem: the lean ramp's uniform-row-0 test (enqueue_fill)
+    for (int64_t j = 0; j < n_all; j++) c->gh_total += cs->gap_h[b_all[j]];
     // one stripe (64 columns) per compute wave; a workgroup (one per CU) chains 4 waves (one per
     // SIMD: the fastest rows) when every stripe gets a wave that way, else 8 (two per SIMD)
     set_stripes(c, c->T_req, false, false);
@@ -710,6 +714,13 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
     p.dbg = c->dbg_on ? c->dbg.as<unsigned long long>() : nullptr;
     // the lane fill's query profile, built on the fill's stream just before it (K x (m + 4) dwords: C5 1.9 MB, a few us).
     // Fills of one problem in flight on other streams (align_many) rewrite it with the same values.
+    // the lean ramp (ga_lane.hip lean0): row 0 is the reference's boundary and uniform in the shifted domain (H' = o,
+    // h2' = 2o in every column: 2o + GH(n) <= big); GA_LANE_LEAN0=0 keeps the masked ramp (A/B)
+    {
+        const char* e = c->knob("GA_LANE_LEAN0");
+        p.lean0 = (e ? atoi(e) : 1) && c->lane && !c->custom && bd.top == nullptr && !bd.band &&
+                  2 * (int64_t)c->o + c->gh_total <= (int64_t)c->big;
+    }
     p.qprof = nullptr;
     if (c->lane && !c->xknob("GA_LANE_QPROF_WAVE")) {  // (experiments build: the profile wave builds it, for A/B)
         HIPCHK(c->qprof.ensure(sizeof(uint32_t) * (size_t)c->K * (size_t)(m + 4)));
@@ -1019,7 +1030,7 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
     if (int r = enqueue_fill(c, 0, pass1)) return r;
     RngTable R;
     const double t1 = now_ms();
-    build_rng(mt_state, m + n + 1, R);
+    build_rng_threaded(mt_state, m + n + 1, R, c->rng_threads);
     c->rng_ms = (float)(now_ms() - t1);
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
     WalkStart st{m, n, 0, 0, 0, 1};
@@ -1397,7 +1408,7 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     // the tie-break table on the host while the device fills
     RngTable R;
     const double t1 = now_ms();
-    build_rng(mt_state, m + n + 1, R);
+    build_rng_threaded(mt_state, m + n + 1, R, c->rng_threads);
     c->rng_ms = (float)(now_ms() - t1);
     WalkBufs wb = ctx_walk_bufs(c);
     const int64_t ntab = (int64_t)R.tab.size();
@@ -2116,6 +2127,9 @@ int ga_ctx_create_opts(int device, const char* options, ga_ctx** out) {
     ga_ctx* c = new ga_ctx();
     c->device = device;
     c->knobs = std::move(knobs);
+    // the tie-break table's threads: up to 8 of the host's (GA_RNG_THREADS, an option; 1: the sequential build)
+    c->rng_threads = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    if (const char* e = c->knob("GA_RNG_THREADS")) c->rng_threads = std::max(1, std::min(64, atoi(e)));
     {
         // hardware queues per priority pool: what the HIP runtime read when it started, i.e. the variable
         // as the process first saw it here (a later change, e.g. a module setting it after HIP started,
@@ -2253,7 +2267,7 @@ int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const
     if (!c->filled_tb) return fail(GA_E_STATE, "traceback needs a GA_FILL_TRACEBACK fill first");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
     RngTable R;
-    build_rng(mt_state, c->m + c->n + 1, R);
+    build_rng_threaded(mt_state, c->m + c->n + 1, R, c->rng_threads);
     if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), WalkStart{c->m, c->n, 0, 0, 0, 1})) return r;
     return finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
 }
@@ -2278,7 +2292,7 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     // the tie-break table is built on the host while the device fills
     RngTable R;
     const double t1 = now_ms();
-    build_rng(mt_state, c->m + c->n + 1, R);
+    build_rng_threaded(mt_state, c->m + c->n + 1, R, c->rng_threads);
     c->rng_ms = (float)(now_ms() - t1);
     if (std::min(c->m, c->n) >= 256 && !c->knob("GA_WALK_NOSTREAM")) {
         // levels to pinned host memory, decoded while the walk runs (as rc_align; degenerate walks, which
@@ -2477,7 +2491,7 @@ int ga_slab_walk_prepare(ga_ctx* c, const uint32_t* mt_state) {
     if (int r = check_ctx(c)) return r;
     if (!mt_state) return fail(GA_E_ARG, "null argument");
     const double t0 = now_ms();
-    build_rng(mt_state, c->m + c->n_global + 1, c->walk_rng);
+    build_rng_threaded(mt_state, c->m + c->n_global + 1, c->walk_rng, c->rng_threads);
     c->rng_ms = (float)(now_ms() - t0);
     c->walk_rng_ready = true;
     return GA_OK;
@@ -2607,6 +2621,19 @@ int ga_debug_rng(const uint32_t* state, int64_t steps, uint32_t* tab_out, int64_
     RngTable R;
     const double t0 = now_ms();
     build_rng(state, steps, R);
+    if (ms_out) *ms_out = now_ms() - t0;
+    std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
+    state_after(R, D, state_out);
+    return GA_OK;
+}
+
+// CPU-only check of the threaded table build (tests): as ga_debug_rng on `threads` host threads.
+int ga_debug_rng_threaded(const uint32_t* state, int64_t steps, int32_t threads, uint32_t* tab_out, int64_t D,
+                          uint32_t* state_out, double* ms_out) {
+    if (!state || !tab_out || !state_out || D < 0 || D > steps || threads < 1) return fail(GA_E_ARG, "bad argument");
+    RngTable R;
+    const double t0 = now_ms();
+    build_rng_threaded(state, steps, R, threads);
     if (ms_out) *ms_out = now_ms() - t0;
     std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
     state_after(R, D, state_out);

@@ -24,8 +24,8 @@ constexpr unsigned LK_DONE = 0x7fffffffu;
 // DBG stamps per stripe (tools/lane_stamps.py): start, end, wait cycles (edges, profile, ring space), total cycles,
 // HW_ID, XCC_ID; the row-m/2 probe: edge row known landed, own row published, (the workgroup's first stripe) landed
 // in ring 0 by the IO wave, (its last stripe) stored to HBM by the out-path
-constexpr int LK_DBG_WORDS = 18;  // + [12] the first edge wait's cycles, [13] when it ended, [14..17] when the
-                                   // wave started the sub-chunk of row 256, 1024, 4096, 16384
+constexpr int LK_DBG_WORDS = 20;  // + [12] the first edge wait's cycles, [13] when it ended, [14..19] when the
+                                   // wave started the sub-chunk of row 256, 1024, 4096, 16384, 64, 128
 typedef unsigned lk_v2u __attribute__((ext_vector_type(2)));
 // waves of a lane-fill workgroup: NWC compute waves, the IO wave, the profile wave and, for NWC <= 4, an out wave that
 // only moves the last compute wave's rows to HBM (at NWC = 8 a third extra wave would put three waves on a SIMD and

@@ -355,12 +355,19 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         if (lane < 3) {
             if (p.qprof) copy_dword(lane - 2);
             else put_dword(lane - 2);
+        } else if (p.lean0) {
+            // the lean ramp (lean0): lanes still above row 1 read the dwords of rows -63 .. -3 too (lane L writes dword
+            // L - 66), all zero bytes, so that their steps keep row 0's values; with dwords -2 .. 0 they fill the ring's
+            // last 64 slots, which rows QR - 63 .. QR reuse only once every wave is past its first 64 steps (below)
+            const unsigned slot = (unsigned)(lane - 67) & qmask;
+            for (int c = 0; c < K; c++) pq[c * QS + slot] = 0u;
         }
         unsigned q_next = 0, spins = 0;
         while (q_next < (unsigned)m) {
-            // the slowest wave reads rows above (its output rows) - 16, so slots of rows below that + QR are free
+            // the slowest wave reads rows above (its output rows) - 16, so slots of rows below that + QR are free;
+            // lean0: until it has published a row (its lanes all past row 0) the ring's last 64 slots hold the zero rows
             const unsigned pl = lds_ld(&cnt[2 * nlive - 1]);
-            const unsigned space = (pl > 32u ? pl - 32u : 0u) + (unsigned)QR;
+            const unsigned space = p.lean0 && pl == 0u ? (unsigned)QR - 64u : (pl > 32u ? pl - 32u : 0u) + (unsigned)QR;
             const unsigned hi = min(min(space, (unsigned)m), q_next + 64);
             if (hi > q_next && (hi - q_next >= 64 || hi == (unsigned)m)) {
                 const unsigned r = q_next + 1 + lane;
@@ -422,7 +429,8 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         }
     }
     int HLp = p.top[min(jl, p.n)].x;  // lane 0: H'(0, j0), the diagonal of row 1
-    int Hl = H[TD - 1], Xl = 0, RH = 0, RX = 0;
+    // (lean0: the h1' a lane above row 1 hands right must not undercut row 0's H' = o, so it starts at 2o)
+    int Hl = H[TD - 1], Xl = p.lean0 ? 2 * o : 0, RH = 0, RX = 0;
     const int2* rin = ring + w * RING;
     int2* rout = ring + (w + 1) * RING;
     // the hand-scheduled asm step (ga_lane_asm.h) for the unmasked sub-chunks of the score-only fills
@@ -466,8 +474,10 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     }
     // DBG: when the wave started the sub-chunks of rows 256, 1024, 4096 and 16384 (how the lag between two stripes
     // grows along the rows: tools/lane_stamps.py "lag_by_row")
-    unsigned long long t_rows[4] = {0, 0, 0, 0};
+    unsigned long long t_rows[6] = {0, 0, 0, 0, 0, 0};
     auto dbg_rows = [&](int r0) {
+        if (r0 == 64) t_rows[4] = __builtin_amdgcn_s_memrealtime();
+        if (r0 == 128) t_rows[5] = __builtin_amdgcn_s_memrealtime();
         if (r0 == 256) t_rows[0] = __builtin_amdgcn_s_memrealtime();
         if (r0 == 1024) t_rows[1] = __builtin_amdgcn_s_memrealtime();
         if (r0 == 4096) t_rows[2] = __builtin_amdgcn_s_memrealtime();
@@ -648,7 +658,8 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                 steps(std::false_type{}, std::false_type{});
             }
         } else {
-            const bool masked = !LEAN && (r0 < 64 || (unsigned)(tm - r0) < (unsigned)SUB);
+            // (lean0, a uniform row 0: the first 64 steps need no mask either, for the asm statement; see it_lo below)
+            const bool masked = !LEAN && ((r0 < 64 && !(p.lean0 && use_asm)) || (unsigned)(tm - r0) < (unsigned)SUB);
             if constexpr (ASMOK) {
                 if (LEAN || (use_asm && !masked && !hand_direct)) {
                     // The lean sub-chunk: the 16 steps, the next sub-chunk's profile and edge reads
@@ -811,7 +822,11 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     int it_lo = nit, it_hi = nit;
     if constexpr (LEANOK) {
         if (use_asm && !hand_direct) {
-            it_lo = min(64 / (2 * SUB), nit);
+            // lean0 (a uniform row 0): from the first iteration.  A lane above row 1 steps on zero profile bytes, so
+            // M' = H'(diag) = o, X' >= o (its left lane's h1', which starts at 2o), Y' = 2o: H' = o, h2' = 2o, h1' in
+            // [o, 2o] -- row 0's values, unchanged, until the lane reaches row 1.  Otherwise the masked ramp first (the
+            // generic path; the first 64 steps of every stripe, on the chain's critical path: round 6)
+            it_lo = p.lean0 ? 0 : min(64 / (2 * SUB), nit);
             // every sub-chunk x of [it_lo, it_hi) has x <= tm - SUB: (unsigned)(tm - x) >= SUB
             it_hi = !partial ? nit : tm - 3 * SUB + 1 >= 0 ? min(nit, (tm - 3 * SUB + 1) / (2 * SUB) + 1) : 0;
             // RC: and no row past m in a lean sub-chunk (its checkpoint store does not test): r0 + SUB - 62 + 15 <= m
@@ -906,7 +921,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
         d[12] = w_first;
         d[13] = t_first;
 #pragma unroll
-        for (int k = 0; k < 4; k++) d[14 + k] = t_rows[k];
+        for (int k = 0; k < 6; k++) d[14 + k] = t_rows[k];
     }
 }
 

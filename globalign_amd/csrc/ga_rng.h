@@ -145,6 +145,8 @@ struct RngTable {
     unsigned d = 0;                   // draw index within the dispatch (0..17)
     std::vector<uint8_t> acc;         // accepted draws (values 0..2)
     int64_t built = 0;                // dispatches whose entries are in tab
+    std::vector<uint32_t> ring;       // build_rng_threaded's scratch: twisted blocks in flight, top-bit quartets
+    std::vector<uint8_t> codes;
 
     void start(const uint32_t* state) {
         std::memcpy(g.mt, state, sizeof(uint32_t) * MTN);
@@ -234,20 +236,21 @@ inline void build_rng(const uint32_t* state, int64_t steps, RngTable& R) {
 }
 
 // The same table on `threads` host threads (round 6: the sequential build took 5.0 ms of one host thread per C3 call,
-// hidden behind the 8.9 ms fill, but on the critical path of any faster fill).  The MT19937 twists stay sequential
-// (each block is the previous one twisted) and cost ~0.15 us a block; everything after them is split into chunks of
-// CHB blocks:
-//   1. (threads, as the twister publishes blocks) temper each word to its top two bits and scan the chunk from every
-//      possible start class -- draw index mod 9: draws d and d + 9 have the same size, so they accept the same words
-//      -- until the nine trajectories meet (a word of top bits 2 accepted at a size-3 draw and rejected at a size-2
-//      one moves them apart or together: they coalesce within a few hundred words), then once: the chunk's accepted
-//      draws and end class for each start class;
-//   2. (one thread, one step per chunk) the true start phase and first accepted draw of every chunk;
-//   3. (threads) rescan each chunk from its known phase, writing the accepted draws and the word count at the end of
-//      every dispatch (step_end), then the dispatch entries (fill_entries).
+// hidden behind the fill, but on the critical path of any faster one).  Its cost is the scan's dependent chain (each
+// four-word lookup needs the draw index the last one left: ~2.5 ns a quartet) more than the MT19937 twists (0.9 ms at
+// C3, sequential by nature: each block of 624 words is the previous one twisted).  So this thread twists, into a ring
+// of blocks, and W = threads - 1 workers each take one contiguous range of blocks, streaming behind it:
+//   1. temper each word to its top two bits and scan the range from every possible start class -- draw index mod 9:
+//      draws d and d + 9 have the same size, so they accept the same words -- until the nine trajectories meet (a
+//      word of top bits 2 is accepted at a size-3 draw and rejected at a size-2 one; they meet within a few hundred
+//      words), then once: the range's accepted draws and end class from each start class;
+//   2. (this thread, once every range is summarized) each range's start phase and first accepted draw;
+//   3. each worker rescans its range from its phase with the sequential scan's branch-free quartet table, writing
+//      the accepted draws and the word count at the end of every dispatch (step_end), then the entries of the
+//      dispatches whose draws it holds; the few straddling two ranges are finished here.
 // The words needed are not known before the scan (32 per dispatch on average, sd 5.2): the twister makes enough for
-// 8 sd above the mean; a shortfall continues sequentially (extend).  The result equals build_rng's, the stream
-// position included, so the table stays resumable.
+// 8 sd above the mean, and a shortfall continues sequentially (extend).  The result equals build_rng's, the stream
+// position included, so the table stays resumable (tests: ga_host_selftest, test_host_cpu).
 struct ClassQuad {
     uint8_t nacc[9][256], ncls[9][256];
     ClassQuad() {
@@ -267,151 +270,173 @@ struct ClassQuad {
 };
 
 inline void build_rng_threaded(const uint32_t* state, int64_t steps, RngTable& R, int threads) {
-    if (threads <= 1 || steps < 4096) return build_rng(state, steps, R);
+    const int W = threads - 1;  // workers beside the twister
+    if (W < 1 || steps < 8192) return build_rng(state, steps, R);
     static const ClassQuad CQ;
-    static const Quad Q;
+    static const Quad2 Q2;
     static const unsigned sz[18] = {3, 2, 2, 2, 3, 2, 2, 2, 3, 3, 2, 2, 2, 3, 2, 2, 2, 3};
-    constexpr int CHB = 8;  // blocks (of 624 words) per chunk
-    R.start(state);         // the initial array, its partial first block (R.words, R.count) and twist_snap[0]
+    constexpr int RINGB = 256;    // twisted blocks in flight
+    constexpr int QPB = MTN / 4;  // quartets per block
+    R.start(state);               // the initial array, its partial first block (R.words, R.count) and twist_snap[0]
     const int first = R.count;
-    // words wanted: 32 per dispatch + 8 sd + slack
     const double sd = 5.2 * std::sqrt((double)steps);
     const int64_t want = 32 * steps + (int64_t)(8 * sd) + 4096;
-    const int64_t nblk = std::max<int64_t>(1, (want - first + MTN - 1) / MTN);  // twisted blocks
-    const int64_t nch = (nblk + CHB - 1) / CHB;
-    std::vector<uint32_t> blocks((size_t)nblk * MTN);  // twisted (untempered) arrays
-    std::vector<uint8_t> codes((size_t)nblk * (MTN / 4));  // top-bit quartets per block
-    std::vector<std::array<int64_t, 9>> ncnt(nch);
-    std::vector<std::array<uint8_t, 9>> ecls(nch);
-    std::atomic<int64_t> made{0}, next_chunk{0};
-    // 1. the twister (this thread) and the chunk scanners
-    auto scan_chunk = [&](int64_t ch) {
-        const int64_t b0 = ch * CHB, b1 = std::min<int64_t>(nblk, b0 + CHB);
-        while (made.load(std::memory_order_acquire) < b1) std::this_thread::yield();
-        for (int64_t b = b0; b < b1; b++) {
-            const uint32_t* mt = &blocks[(size_t)b * MTN];
-            uint8_t* cd = &codes[(size_t)b * (MTN / 4)];
-            for (int k = 0; k < MTN / 4; k++) {
-                unsigned B = 0;
-                for (int w = 0; w < 4; w++) {
-                    uint32_t y = mt[4 * k + w];
-                    y ^= (y >> 11);
-                    y ^= (y << 7) & 0x9d2c5680u;
-                    y ^= (y << 15) & 0xefc60000u;
-                    y ^= (y >> 18);
-                    B |= (y >> 30) << (2 * w);
-                }
-                cd[k] = (uint8_t)B;
-            }
+    const int64_t nblk = std::max<int64_t>(W, (want - first + MTN - 1) / MTN);  // twisted blocks
+    R.ring.resize((size_t)RINGB * MTN);      // (scratch kept by the table: no page faults when it is reused)
+    R.codes.resize((size_t)nblk * QPB);
+    struct alignas(64) Range {
+        int64_t b0 = 0, b1 = 0;               // blocks [b0, b1)
+        int64_t cnt[9] = {};                  // accepted draws from each start class
+        uint8_t ecls[9] = {};                 // end class from each start class
+        int64_t p0 = 0, p1 = 0;               // its draws [p0, p1)
+        unsigned d0 = 0;                      // its start phase
+        std::atomic<int64_t> tempered{0};     // blocks done (the twister may reuse their ring slots)
+    };
+    std::vector<Range> rg(W);
+    for (int w = 0; w < W; w++) {
+        rg[w].b0 = nblk * w / W;
+        rg[w].b1 = nblk * (w + 1) / W;
+    }
+    // the partial first block from phase 0, word by word
+    int64_t p = 0;
+    unsigned d = 0;
+    const size_t max_draws = (size_t)first + (size_t)nblk * MTN + 8;
+    if (R.acc.size() < max_draws) R.acc.resize(max_draws);
+    if (R.step_end.size() < max_draws / 18 + 8) R.step_end.resize(max_draws / 18 + 8);
+    if (R.tab.size() < (size_t)steps) R.tab.resize(steps);
+    uint8_t* acc = R.acc.data();
+    uint32_t* se = R.step_end.data();
+    for (int w = 0; w < first; w++) {
+        const unsigned r = R.words[w] >> 30;
+        if (r < sz[d]) {
+            acc[p] = (uint8_t)r;
+            if (d == 17) se[p / 18] = (uint32_t)(w + 1);
+            p++;
+            d = d == 17 ? 0 : d + 1;
         }
-        const uint8_t* cd = &codes[(size_t)b0 * (MTN / 4)];
-        const int64_t nq = (b1 - b0) * (MTN / 4);
+    }
+    const int64_t p_head = p;
+    std::atomic<int64_t> made{0};
+    std::atomic<int> phase{0};  // 1: every range has its start (phase 3 may run)
+    auto spin = [](int& k) {
+        if (++k > 64) std::this_thread::yield();
+    };
+    auto worker = [&](int w) {
+        Range& G = rg[w];
+        uint8_t* cd = R.codes.data();
+        // 1. temper + summary, streaming behind the twister
         int64_t cnt[9];
         uint8_t cls[9];
         for (int c = 0; c < 9; c++) {
             cnt[c] = 0;
             cls[c] = (uint8_t)c;
         }
-        int64_t k = 0;
         bool met = false;
-        for (; k < nq && !met; k++) {
-            const unsigned B = cd[k];
-            met = true;
-            for (int c = 0; c < 9; c++) {
-                cnt[c] += CQ.nacc[cls[c]][B];
-                cls[c] = CQ.ncls[cls[c]][B];
-            }
-            for (int c = 1; c < 9; c++) met &= cls[c] == cls[0];
-        }
         int64_t shared = 0;
-        uint8_t c0 = cls[0];
-        for (; k < nq; k++) {
-            const unsigned B = cd[k];
-            shared += CQ.nacc[c0][B];
-            c0 = CQ.ncls[c0][B];
+        for (int64_t b = G.b0; b < G.b1; b++) {
+            for (int k = 0; made.load(std::memory_order_acquire) <= b;) spin(k);
+            const uint32_t* mt = &R.ring[(size_t)(b % RINGB) * MTN];
+            uint8_t* cb = cd + b * QPB;
+            for (int q = 0; q < QPB; q++) {
+                unsigned B = 0;
+                for (int x = 0; x < 4; x++) {
+                    uint32_t y = mt[4 * q + x];
+                    y ^= (y >> 11);
+                    y ^= (y << 7) & 0x9d2c5680u;
+                    y ^= (y << 15) & 0xefc60000u;
+                    y ^= (y >> 18);
+                    B |= (y >> 30) << (2 * x);
+                }
+                cb[q] = (uint8_t)B;
+            }
+            G.tempered.store(b + 1 - G.b0, std::memory_order_release);
+            if (!met) {
+                for (int q = 0; q < QPB; q++) {
+                    const unsigned B = cb[q];
+                    if (met) {
+                        shared += CQ.nacc[cls[0]][B];
+                        cls[0] = CQ.ncls[cls[0]][B];
+                        continue;
+                    }
+                    for (int c = 0; c < 9; c++) {
+                        cnt[c] += CQ.nacc[cls[c]][B];
+                        cls[c] = CQ.ncls[cls[c]][B];
+                    }
+                    met = true;
+                    for (int c = 1; c < 9; c++) met &= cls[c] == cls[0];
+                }
+            } else {
+                uint8_t c0 = cls[0];
+                for (int q = 0; q < QPB; q++) {
+                    shared += CQ.nacc[c0][cb[q]];
+                    c0 = CQ.ncls[c0][cb[q]];
+                }
+                cls[0] = c0;
+            }
         }
         for (int c = 0; c < 9; c++) {
-            ncnt[ch][c] = cnt[c] + shared;
-            ecls[ch][c] = met ? c0 : cls[c];
+            G.cnt[c] = cnt[c] + shared;
+            G.ecls[c] = met ? cls[0] : cls[c];
         }
+        G.tempered.store(G.b1 - G.b0 + 1, std::memory_order_release);  // (one past: the summary is in)
+        // 3. once every start is known: the draws and dispatch ends, then the entries inside the range
+        for (int k = 0; phase.load(std::memory_order_acquire) == 0;) spin(k);
+        int64_t pp = G.p0, stp = pp / 18;
+        unsigned dd = G.d0;
+        uint32_t spill = 0;  // the step_end store of a quartet that completes no dispatch
+        const int64_t nq = (G.b1 - G.b0) * QPB;
+        const uint8_t* cr = cd + G.b0 * QPB;
+        const int64_t wb = first + G.b0 * MTN;  // the range's first word, counted from the stream's start
+        for (int64_t q = 0; q < nq; q++) {
+            const QuadEntry2& e = Q2.e[dd][cr[q]];
+            if (pp + 4 <= G.p1) std::memcpy(acc + pp, &e.bytes, 4);  // (junk past the accepted bytes: overwritten)
+            else
+                for (unsigned t = 0; t < e.nacc; t++) acc[pp + t] = (uint8_t)(e.bytes >> (8 * t));
+            *(e.wrap ? se + stp : &spill) = (uint32_t)(wb + 4 * q + e.woff);
+            stp += e.wrap;
+            pp += e.nacc;
+            dd = e.nd;
+        }
+        const int64_t lo = (G.p0 + 17) / 18, hi = std::min<int64_t>(G.p1 / 18, steps);
+        if (lo < hi) fill_entries(acc, lo, hi, R);
     };
-    auto worker1 = [&]() {
-        for (int64_t ch; (ch = next_chunk.fetch_add(1)) < nch;) scan_chunk(ch);
-    };
-    const int nw = std::max(1, threads - 1);
     std::vector<std::thread> pool;
-    for (int t = 0; t < nw; t++) pool.emplace_back(worker1);
+    pool.reserve(W);
+    for (int w = 0; w < W; w++) pool.emplace_back(worker, w);
+    // the twister: this thread (snapshots every TWSNAP twists, as extend() takes them)
     PyMT g = R.g;
+    int owner = 0;  // the range of block b
     for (int64_t b = 0; b < nblk; b++) {
+        while (owner + 1 < W && b >= rg[owner + 1].b0) owner++;
+        if (b >= RINGB) {  // block b reuses block b - RINGB's slot: wait until its range has tempered it
+            const int64_t old = b - RINGB;
+            int ow = owner;
+            while (rg[ow].b0 > old) ow--;
+            for (int k = 0; rg[ow].tempered.load(std::memory_order_acquire) <= old - rg[ow].b0;) spin(k);
+        }
         g.twist();
         if ((b + 1) % TWSNAP == 0) R.twist_snap.push_back(g);
-        std::memcpy(&blocks[(size_t)b * MTN], g.mt, sizeof(uint32_t) * MTN);
+        std::memcpy(&R.ring[(size_t)(b % RINGB) * MTN], g.mt, sizeof(uint32_t) * MTN);
         made.store(b + 1, std::memory_order_release);
     }
-    for (auto& t : pool) t.join();
-    pool.clear();
-    // 2. stitch: the partial first block from phase 0 (word by word), then chunk by chunk
-    int64_t p = 0;
-    unsigned d = 0;
-    std::vector<uint8_t> acc0;
-    std::vector<uint32_t> end0;
-    for (int w = 0; w < first; w++) {
-        const unsigned r = R.words[w] >> 30;
-        if (r < sz[d]) {
-            acc0.push_back((uint8_t)r);
-            if (d == 17) end0.push_back((uint32_t)(w + 1));
-            p++;
-            d = d == 17 ? 0 : d + 1;
-        }
-    }
-    std::vector<int64_t> pstart(nch + 1);
-    std::vector<uint8_t> dstart(nch + 1);
-    for (int64_t ch = 0; ch < nch; ch++) {
-        pstart[ch] = p;
-        dstart[ch] = (uint8_t)d;
+    // 2. the ranges' starts, in order, once their summaries are in
+    p = p_head;
+    for (int w = 0; w < W; w++) {
+        for (int k = 0; rg[w].tempered.load(std::memory_order_acquire) <= rg[w].b1 - rg[w].b0;) spin(k);
         const int c = (int)(d % 9);
-        p += ncnt[ch][c];
-        // the end phase: the end class, in the half (0..8 or 9..17) that the draws counted land in
-        const unsigned e = ecls[ch][c];
-        d = (unsigned)((d + ncnt[ch][c]) % 18);
-        if (d % 9 != e) {  // cannot happen: the class arithmetic is the phase arithmetic mod 9
-            R = RngTable();
-            return build_rng(state, steps, R);
-        }
+        rg[w].p0 = p;
+        rg[w].d0 = d;
+        p += rg[w].cnt[c];
+        d = (unsigned)((d + rg[w].cnt[c]) % 18);
+        rg[w].p1 = p;
     }
-    pstart[nch] = p;
-    dstart[nch] = (uint8_t)d;
-    const int64_t total = p, ndisp = total / 18;
-    // 3. the accepted draws and dispatch ends, chunk by chunk from known phases
-    R.acc.assign((size_t)total + 8, 0);
-    R.step_end.assign((size_t)std::max<int64_t>(ndisp, steps) + 4, 0);
-    std::memcpy(R.acc.data(), acc0.data(), acc0.size());
-    for (size_t k = 0; k < end0.size(); k++) R.step_end[k] = end0[k];
-    next_chunk.store(0);
-    auto worker3 = [&]() {
-        for (int64_t ch; (ch = next_chunk.fetch_add(1)) < nch;) {
-            const int64_t b0 = ch * CHB, b1 = std::min<int64_t>(nblk, b0 + CHB);
-            const uint8_t* cd = &codes[(size_t)b0 * (MTN / 4)];
-            const int64_t nq = (b1 - b0) * (MTN / 4);
-            int64_t pp = pstart[ch];
-            unsigned dd = dstart[ch];
-            const int64_t wb = first + b0 * MTN;  // global index of the chunk's first word
-            for (int64_t k = 0; k < nq; k++) {
-                const unsigned B = cd[k];
-                const QuadEntry& e = Q.e[dd][B];
-                const unsigned na = e.meta & 7u;
-                for (unsigned t = 0; t < na; t++) {
-                    R.acc[(size_t)pp] = (uint8_t)((e.bytes >> (8 * t)) & 0xffu);
-                    if (dd == 17) R.step_end[(size_t)(pp / 18)] = (uint32_t)(wb + 4 * k + ((e.meta >> (3 + 2 * t)) & 3u) + 1);
-                    pp++;
-                    dd = dd == 17 ? 0 : dd + 1;
-                }
-            }
-        }
-    };
-    for (int t = 0; t < threads; t++) pool.emplace_back(worker3);
+    phase.store(1, std::memory_order_release);
     for (auto& t : pool) t.join();
-    pool.clear();
+    const int64_t total = p, ndisp = total / 18;
+    // the entries no range holds whole: inside the partial first block, and those straddling two ranges
+    fill_entries(acc, 0, std::min<int64_t>(steps, p_head / 18), R);
+    for (int w = 0; w < W; w++)
+        if (rg[w].p0 % 18 && rg[w].p0 / 18 < steps) fill_entries(acc, rg[w].p0 / 18, rg[w].p0 / 18 + 1, R);
     // the stream position after every generated word (resumable: extend continues from here)
     R.g = g;
     temper_block(g.mt, R.words);
@@ -422,19 +447,14 @@ inline void build_rng_threaded(const uint32_t* state, int64_t steps, RngTable& R
     R.p = total;
     R.stp = ndisp;
     R.d = d;
+    R.acc.resize((size_t)total + 8);
     if (ndisp < steps) {  // the twister fell short (8 sd): continue sequentially
-        R.built = 0;
+        R.built = std::min<int64_t>(ndisp, steps);
+        R.tab.resize(R.built);
         R.extend(steps);
         return;
     }
-    // the dispatch entries
     R.tab.resize(steps);
-    const int64_t per = (steps + threads - 1) / threads;
-    for (int t = 0; t < threads; t++) {
-        const int64_t lo = t * per, hi = std::min(steps, lo + per);
-        if (lo < hi) pool.emplace_back([&R, lo, hi]() { fill_entries(R.acc.data(), lo, hi, R); });
-    }
-    for (auto& t : pool) t.join();
     R.built = steps;
 }
 

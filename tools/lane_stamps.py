@@ -43,7 +43,7 @@ plain_ms = eng.kernel_ms()[0]
 L.ga_debug_stamps(eng._h, 1, None, 0)
 cost, _ = eng.fill(traceback=False)
 kind, T, ns, nwc, nslabs = eng.fill_kind()
-W = 18  # LK_DBG_WORDS (ga_lane.h)
+W = 20  # LK_DBG_WORDS (ga_lane.h)
 buf = np.zeros(W * ns, dtype=np.uint64)
 L.ga_debug_stamps(eng._h, 0, buf.ctypes.data, buf.size)
 L.ga_debug_stamps(eng._h, 0, None, 0)
@@ -84,6 +84,10 @@ steady = {"wait_edge_first_frac_median": float(np.median(first_w / tot)),
           "ns_per_step_after_first_edge_median": float(np.median(steady_ns)),
           "ns_per_step_after_first_edge_by_decile": [float(np.median(steady_ns[d])) for d in dec],
           "cyc_per_step_after_first_edge_median": float(np.median((tot - first_w) / (m + 63)))}
+# the first 64 steps (the ramp's masked sub-chunks, or the lean ones with lean0) against the next 64 (words 18, 19)
+if (st[:, 18] > 0).all() and (st[:, 19] > 0).all():
+    steady["ns_per_step_first64_median"] = float(np.median((st[:, 18] - st[:, 13]) * 10.0 / 64))
+    steady["ns_per_step_next64_median"] = float(np.median((st[:, 19] - st[:, 18]) * 10.0 / 64))
 # the lag between consecutive stripes at rows 256 / 1024 / 4096 / 16384 (words 14..17), intra- and cross-workgroup
 # links apart: a link's lag is set where it first grows (a consumer never catches up), DESIGN.md 5.6.2
 lag_by_row = {}
