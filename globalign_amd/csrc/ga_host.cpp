@@ -126,7 +126,14 @@ struct ga_ctx {
     int64_t n_global = 0, col0 = 0;
     int K = 0, o = 0, big = 0, CB = 1, qbytes = 1;
     int64_t gh_total = 0;      // GH(n_global): the sum of the horizontal gap costs of seq_2
-    int rng_threads = 1;       // host threads building a call's tie-break table (ga_rng.h build_rng_threaded)
+    int64_t gv_total = 0;      // GV(m): the sum of the vertical gap costs of seq_1
+    // a streamed single call's small results in pinned, coherent host memory (no copy after the walk): [0, 16) the
+    // walk's result words (it writes them there), [16, 20) the fill's H'(m, n) words, [20] its abort word (copied on
+    // the upload stream while the walk runs); res_dev: the same memory as the device sees it
+    int* res_pin = nullptr;
+    int* res_dev = nullptr;
+    hipEvent_t ev_fill = nullptr, ev_res = nullptr;
+    bool rc_pos_zeroed = false;  // rc_pos was cleared on the fill's stream before the fill (rc_align)
     int nstripes = 0, nslabs = 0, TC = 0, nwc = 4, qrows = 1024, num_cu = 256;
     int T = 1, T_req = 0, nwc_req = 0;
     int diag_req = 0;          // score-only fill kernel: 0 automatic, 1 row scan, 2 anti-diagonal, 3 lane-skewed (GA_FILL_MODE)
@@ -357,8 +364,10 @@ int load_problem(ga_ctx* c, const uint8_t* a, int64_t m, const uint8_t* b_all, i
     c->o = o;
     c->big = (int)big;
     c->custom = row0 != nullptr || col0 != nullptr;
-    c->gh_total = 0;  // GH(n) of the whole problem: the lean ramp's uniform-row-0 test (enqueue_fill)
+    c->gh_total = 0;  // GH(n) of the whole problem: the lean ramp's uniform-row-0 test (enqueue_fill), the cost
     for (int64_t j = 0; j < n_all; j++) c->gh_total += cs->gap_h[b_all[j]];
+    c->gv_total = 0;  // GV(m): the cost's un-shift (cost = H'(m, n) + GV(m) + GH(n))
+    for (int64_t i = 0; i < m; i++) c->gv_total += cs->gap_v[a[i]];
     // one stripe (64 columns) per compute wave; a workgroup (one per CU) chains 4 waves (one per
     // SIMD: the fastest rows) when every stripe gets a wave that way, else 8 (two per SIMD)
     set_stripes(c, c->T_req, false, false);
@@ -1030,7 +1039,7 @@ int banded_align(ga_ctx* c, int64_t Bh, uint32_t* mt_state, const char* a_chr, c
     if (int r = enqueue_fill(c, 0, pass1)) return r;
     RngTable R;
     const double t1 = now_ms();
-    build_rng_threaded(mt_state, m + n + 1, R, c->rng_threads);
+    build_rng(mt_state, m + n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
     if (int r = finish_fill(c, cost_out, nullptr)) return r;
     WalkStart st{m, n, 0, 0, 0, 1};
@@ -1143,7 +1152,8 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     }
     c->rc_epoch++;
     HIPCHK(c->rc_pos.ensure(16));
-    HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, wb.stream));
+    if (!c->rc_pos_zeroed) HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, wb.stream));
+    c->rc_pos_zeroed = false;
     wb.tb = c->rc_tb.as<uint8_t>();
     ga::WalkArgs w = walk_args(c, ntab, st, 0, -1, false, wb);
     w.TC = ga::RC_CACHE_I * 4 * CB;  // 16-byte words per lane per 64-column stripe of the cache
@@ -1295,6 +1305,43 @@ int pinned_walk_levels(ga_ctx* c, WalkBufs& wb) {
         HIPCHK(hipHostGetDevicePointer(&dp, c->rc_ops_prog, 0));
         wb.ops_prog = static_cast<unsigned*>(dp);
     }
+    // the walk's result words to pinned memory too: no hipMemcpy after the walk (round 6: the call's tail after the
+    // walk held five small copies, ~0.1 ms)
+    if (!c->res_pin) {
+        void* hp = nullptr;
+        HIPCHK(hipHostMalloc(&hp, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        c->res_pin = static_cast<int*>(hp);
+        void* dp = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dp, hp, 0));
+        c->res_dev = static_cast<int*>(dp);
+    }
+    std::memset(c->res_pin, 0, 64 * sizeof(int));
+    wb.result = c->res_dev;
+    return GA_OK;
+}
+
+// The fill's result words (H'(m, n), the abort word) copied to pinned memory on the upload stream as soon as the
+// fill ends, beside the walk (not on the fill's stream, where the copies would delay the walk's start), and read
+// after the walk with no further copy; the cost's un-shift GV(m) + GH(n) comes from the host's own sums.
+int fill_results_async(ga_ctx* c) {
+    if (!c->ustream) HIPCHK(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, c->priority));
+    if (!c->ev_fill) HIPCHK(hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming));
+    if (!c->ev_res) HIPCHK(hipEventCreateWithFlags(&c->ev_res, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->ev_fill, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->ustream, c->ev_fill, 0));
+    HIPCHK(hipMemcpyAsync(c->res_pin + 16, c->out_last.p, sizeof(int) * 4, hipMemcpyDeviceToHost, c->ustream));
+    HIPCHK(hipMemcpyAsync(c->res_pin + 20, c->flags.as<unsigned>() + 1, sizeof(unsigned), hipMemcpyDeviceToHost,
+                          c->ustream));
+    HIPCHK(hipEventRecord(c->ev_res, c->ustream));
+    return GA_OK;
+}
+
+int fill_results_finish(ga_ctx* c, int64_t* cost_out) {
+    HIPCHK(hipEventSynchronize(c->ev_res));
+    HIPCHK(hipEventElapsedTime(&c->fill_ms, c->ev[0], c->ev[1]));
+    if (c->res_pin[20]) return fail(GA_E_TIMEOUT, "fill kernel hand-off wait timed out");
+    c->GV_m = (int)c->gv_total;
+    if (cost_out) *cost_out = (int64_t)c->res_pin[16] + c->gv_total + c->gh_total;
     return GA_OK;
 }
 
@@ -1349,10 +1396,11 @@ int streamed_walk_finish(ga_ctx* c, const RngTable& R, const WalkBufs& wb, const
             if (q != hipErrorNotReady) return fail(GA_E_HIP, std::string("walk: ") + hipGetErrorString(q));
             std::this_thread::yield();
         }
-        // the fill ran before the walk on the same stream: its cost (and any abort) now, with no wait
-        if (int rr = finish_fill(c, cost_out, nullptr)) return rr;
+        // the fill's cost and abort word (copied to pinned memory while the walk ran) and the walk's result words
+        // (written to pinned memory by the walk): no copy here
+        if (int rr = fill_results_finish(c, cost_out)) return rr;
         int res[16];
-        HIPCHK(hipMemcpy(res, wb.result, sizeof(res), hipMemcpyDeviceToHost));
+        std::memcpy(res, c->res_pin, sizeof(res));
         HIPCHK(hipEventElapsedTime(&c->walk_ms, wb.ev0, wb.ev1));
         c->walk_waits = res[4];
         c->walk_tiles = res[5];
@@ -1404,11 +1452,18 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
              int64_t cap, int64_t* out_len, int32_t* tb_status, int64_t* cost_out) {
     const double t0 = now_ms();
     const int64_t m = c->m, n = c->n;
-    if (int r = rc_fill(c)) return r;
+    // the walk's position words cleared before the fill (a memset between the fill and the walk delayed the walk)
+    HIPCHK(c->rc_pos.ensure(16));
+    HIPCHK(hipMemsetAsync(c->rc_pos.p, 0, 16, c->stream));
+    if (int r = rc_fill(c)) {
+        c->rc_pos_zeroed = false;
+        return r;
+    }
+    c->rc_pos_zeroed = true;
     // the tie-break table on the host while the device fills
     RngTable R;
     const double t1 = now_ms();
-    build_rng_threaded(mt_state, m + n + 1, R, c->rng_threads);
+    build_rng(mt_state, m + n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
     WalkBufs wb = ctx_walk_bufs(c);
     const int64_t ntab = (int64_t)R.tab.size();
@@ -1432,6 +1487,8 @@ int rc_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const char* b_chr
     HIPCHK(hipStreamWaitEvent(wb.stream, c->ev_up, 0));
     // the walk's levels go to pinned host memory, and this thread decodes them while the walk runs
     if (int r = pinned_walk_levels(c, wb)) return r;
+    // (after the table's upload on the same side stream: the copies there wait for the fill's end)
+    if (int r = fill_results_async(c)) return r;
     const WalkStart st0{m, n, 0, 0, 0, 1};
     if (int r = rc_walk_launch(c, ntab, st0, wb)) return r;
     return streamed_walk_finish(c, R, wb, st0, t0, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status, cost_out);
@@ -2127,9 +2184,6 @@ int ga_ctx_create_opts(int device, const char* options, ga_ctx** out) {
     ga_ctx* c = new ga_ctx();
     c->device = device;
     c->knobs = std::move(knobs);
-    // the tie-break table's threads: up to 8 of the host's (GA_RNG_THREADS, an option; 1: the sequential build)
-    c->rng_threads = (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
-    if (const char* e = c->knob("GA_RNG_THREADS")) c->rng_threads = std::max(1, std::min(64, atoi(e)));
     {
         // hardware queues per priority pool: what the HIP runtime read when it started, i.e. the variable
         // as the process first saw it here (a later change, e.g. a module setting it after HIP started,
@@ -2196,6 +2250,9 @@ void ga_ctx_destroy(ga_ctx* c) {
     if (c->rc_ops_prog) (void)hipHostFree(c->rc_ops_prog);
     if (c->up_pin) (void)hipHostFree(c->up_pin);
     if (c->ev_up) (void)hipEventDestroy(c->ev_up);
+    if (c->res_pin) (void)hipHostFree(c->res_pin);
+    if (c->ev_fill) (void)hipEventDestroy(c->ev_fill);
+    if (c->ev_res) (void)hipEventDestroy(c->ev_res);
     if (c->ustream) (void)hipStreamDestroy(c->ustream);
     for (auto& sl : c->pipe) {
         for (DevBuf* b : {&sl.tb, &sl.hand, &sl.flags, &sl.out_last, &sl.rng, &sl.ops, &sl.result, &sl.GVp, &sl.GHp,
@@ -2267,7 +2324,7 @@ int ga_problem_traceback(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const
     if (!c->filled_tb) return fail(GA_E_STATE, "traceback needs a GA_FILL_TRACEBACK fill first");
     if (!mt_state || !a_chr || !b_chr || !oa || !om || !ob || !out_len || !tb_status) return fail(GA_E_ARG, "null argument");
     RngTable R;
-    build_rng_threaded(mt_state, c->m + c->n + 1, R, c->rng_threads);
+    build_rng(mt_state, c->m + c->n + 1, R);
     if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), WalkStart{c->m, c->n, 0, 0, 0, 1})) return r;
     return finish_walk(c, R, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status);
 }
@@ -2292,13 +2349,14 @@ int ga_problem_align(ga_ctx* c, uint32_t* mt_state, const char* a_chr, const cha
     // the tie-break table is built on the host while the device fills
     RngTable R;
     const double t1 = now_ms();
-    build_rng_threaded(mt_state, c->m + c->n + 1, R, c->rng_threads);
+    build_rng(mt_state, c->m + c->n + 1, R);
     c->rng_ms = (float)(now_ms() - t1);
     if (std::min(c->m, c->n) >= 256 && !c->knob("GA_WALK_NOSTREAM")) {
         // levels to pinned host memory, decoded while the walk runs (as rc_align; degenerate walks, which
         // need a row or column of the matrix of length 1, keep the plain path)
         WalkBufs wb = ctx_walk_bufs(c);
         if (int r = pinned_walk_levels(c, wb)) return r;
+        if (int r = fill_results_async(c)) return r;
         const WalkStart st0{c->m, c->n, 0, 0, 0, 1};
         if (int r = run_walk(c, R.tab.data(), (int64_t)R.tab.size(), st0, 0, -1, false, true, &wb)) return r;
         return streamed_walk_finish(c, R, wb, st0, t0, mt_state, a_chr, b_chr, oa, om, ob, cap, out_len, tb_status,
@@ -2491,7 +2549,7 @@ int ga_slab_walk_prepare(ga_ctx* c, const uint32_t* mt_state) {
     if (int r = check_ctx(c)) return r;
     if (!mt_state) return fail(GA_E_ARG, "null argument");
     const double t0 = now_ms();
-    build_rng_threaded(mt_state, c->m + c->n_global + 1, c->walk_rng, c->rng_threads);
+    build_rng(mt_state, c->m + c->n_global + 1, c->walk_rng);
     c->rng_ms = (float)(now_ms() - t0);
     c->walk_rng_ready = true;
     return GA_OK;
@@ -2621,19 +2679,6 @@ int ga_debug_rng(const uint32_t* state, int64_t steps, uint32_t* tab_out, int64_
     RngTable R;
     const double t0 = now_ms();
     build_rng(state, steps, R);
-    if (ms_out) *ms_out = now_ms() - t0;
-    std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
-    state_after(R, D, state_out);
-    return GA_OK;
-}
-
-// CPU-only check of the threaded table build (tests): as ga_debug_rng on `threads` host threads.
-int ga_debug_rng_threaded(const uint32_t* state, int64_t steps, int32_t threads, uint32_t* tab_out, int64_t D,
-                          uint32_t* state_out, double* ms_out) {
-    if (!state || !tab_out || !state_out || D < 0 || D > steps || threads < 1) return fail(GA_E_ARG, "bad argument");
-    RngTable R;
-    const double t0 = now_ms();
-    build_rng_threaded(state, steps, R, threads);
     if (ms_out) *ms_out = now_ms() - t0;
     std::memcpy(tab_out, R.tab.data(), sizeof(uint32_t) * steps);
     state_after(R, D, state_out);

@@ -1303,7 +1303,9 @@ void launch_boundary(hipStream_t s, const uint8_t* a, int m, const uint8_t* b, i
         custom_boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, GVp, GHp, top, left, bnd_row, bnd_col, meta);
         return;
     }
-    if ((long long)m + n < 64 * 1024) {  // small problems: one workgroup does it all
+    // small problems: one workgroup does it all (its threads' serial segments read strided codes: C5's 40k codes took
+    // 55 us that way against ~15 for the spread kernels below, round 6)
+    if ((long long)m + n < 4 * 1024) {
         boundary_kernel<<<1, 1024, 0, s>>>(a, m, b, n, gh, gv, o, big, GVp, GHp, top, left, bnd_row, bnd_col, meta);
         return;
     }

@@ -88,6 +88,7 @@ class Links:
         self.device_tensors = backend != "gloo"
         self.ipc_ok = None  # edge links through IPC: agreed by every rank on the first problem (ipc_agreed)
         self.ipc_linked_now = False
+        self.ipc_error = None  # this rank's reason when its link failed
 
     def warm_up(self, dist, torch, device):
         """Create the pair communicators now (one tiny exchange each way on every pair group).
@@ -222,12 +223,47 @@ def ipc_agreed(dist, links, engine):
         except Exception as e:  # noqa: BLE001 (any failure to link falls back, reported on stderr)
             import sys
             print(f"rank {links.rank}: IPC edge link failed ({e}); using bands", file=sys.stderr, flush=True)
+            links.ipc_error = f"{type(e).__name__}: {e}"
             ok = 0
         flag = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=links.ctrl)
         links.ipc_ok = bool(int(flag[0]))
         links.ipc_linked_now = links.ipc_ok  # this problem is already linked
     return links.ipc_ok
+
+
+def edge_preflight(dist, links, engine, a_codes, b_codes, tables):
+    """bench.py --gpus N, before any timed step: load this rank's slab and link its edges (ipc_agreed: every rank
+    tries its IPC links, and a failure on any makes all of them use bands), then report, for each slab boundary,
+    which GPUs it joins and which transport carries its edge -- so that a fallback is visible in the bench line,
+    not only on stderr.  The first step reuses the links.  Collective over all ranks."""
+    rank, world = links.rank, links.world
+    edges = slab_bounds(len(b_codes), world)
+    engine.load_slab(a_codes, b_codes, tables, edges[rank], edges[rank + 1])
+    requested = edge_mode(engine)
+    ipc = requested == "ipc" and ipc_agreed(dist, links, engine)
+    dev = getattr(engine, "device", None)
+    pci = None
+    if dev is not None:
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(dev)
+            pci = "%04x:%02x:%02x" % (getattr(pr, "pci_domain_id", 0), getattr(pr, "pci_bus_id", 0),
+                                      getattr(pr, "pci_device_id", 0))
+        except Exception:  # noqa: BLE001 (diagnostic only)
+            pci = None
+    info = {"rank": rank, "device": dev, "pci": pci, "ipc_error": links.ipc_error}
+    everyone = [None] * world
+    dist.all_gather_object(everyone, info, group=links.ctrl)
+    bounds = []
+    for k in range(world - 1):
+        a, b = everyone[k], everyone[k + 1]
+        bounds.append({"ranks": [k, k + 1], "devices": [a["device"], b["device"]], "pci": [a["pci"], b["pci"]],
+                       "same_gpu": a["pci"] is not None and a["pci"] == b["pci"],
+                       "transport": "ipc (the left fill stores into the right GPU's memory)" if ipc else
+                       "bands (host-relayed halo bands over the process group)"})
+    return {"requested": requested, "ipc_agreed": bool(ipc),
+            "ipc_errors": {e["rank"]: e["ipc_error"] for e in everyone if e["ipc_error"]}, "boundaries": bounds}
 
 
 def link_ipc(dist, links, engine):
@@ -531,6 +567,8 @@ def bench_main(args, wl, workload):
     random.seed(0)
     mt0 = np.array(random.getstate()[1], dtype=np.uint32)
     engine = _bench_engine(tables, local)
+    # the edge links, opened and reported before timing (a fallback to bands shows in the line)
+    preflight = edge_preflight(dist, links, engine, a_codes, b_codes, tables)
     if links.device_tensors:
         links.warm_up(dist, torch, engine.torch_device())
     result = None
@@ -580,11 +618,12 @@ def bench_main(args, wl, workload):
             "data": "synthetic (SplitMix64, SURVEY 8d)",
             "config": {"workload": f"{wl['desc']}; {world} column slabs, "
                                    + ("edges stored by each fill into the next GPU's memory (IPC-mapped, xGMI)"
-                                      if edge_mode(engine) == "ipc" else f"banded RCCL edge exchange ({band}-row bands)")
+                                      if preflight["ipc_agreed"] else f"banded RCCL edge exchange ({band}-row bands)")
                                    + ("; right-to-left walk hand-off" if wl["traceback"] else ""),
                        "m": m, "n": n, "traceback": wl["traceback"], "parallelism": f"column slabs x{world}",
                        "backend": dist.get_backend(), "cost": int(cost), "oracle_cost": gold,
-                       "cost_matches_oracle": (int(cost) == gold) if gold is not None else None},
+                       "cost_matches_oracle": (int(cost) == gold) if gold is not None else None,
+                       "edge_links": preflight},
             # every rank's slab fill is one persistent launch; its time (HIP events, max over ranks)
             # includes the pipeline wait for the left neighbour's first band
             "slab_fill_ms_max": fill_max,

@@ -36,6 +36,10 @@ def test_bench_spawns_ranks_gloo(n):
     assert line["config"]["cost"] == 2471 and line["config"]["backend"] == "gloo"
     assert line["value"] > 0 and line["slab_fill_ms_max"] > 0
     assert sum(line["slab_columns"]) == 1000
+    # the edge preflight: every boundary's transport in the line (CPU engines relay bands)
+    pre = line["config"]["edge_links"]
+    assert len(pre["boundaries"]) == n - 1 and not pre["ipc_agreed"]
+    assert all(b["transport"].startswith("bands") for b in pre["boundaries"])
 
 
 def test_bench_refuses_missing_gpus():

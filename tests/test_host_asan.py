@@ -1,6 +1,6 @@
-"""The engine's host-only pieces under AddressSanitizer + UndefinedBehaviorSanitizer and under ThreadSanitizer (SURVEY 5:
-a sanitizer build of the host C++), no GPU: globalign_amd/csrc/ga_host_selftest.cpp checks the tie-break table (ga_rng.h: the four-word
-scan, the resumable stream, the threaded build, the state after D dispatches) against a draw-by-draw restatement of
+"""The engine's host-only pieces under AddressSanitizer + UndefinedBehaviorSanitizer (a sanitizer build of
+the host C++), no GPU: globalign_amd/csrc/ga_host_selftest.cpp checks the tie-break table (ga_rng.h: the four-word
+scan, the resumable stream, the state after D dispatches) against a draw-by-draw restatement of
 CPython's random.choice, and the problem checks (ga_check.h: validation, the int32 range guard, word widths).  The same
 binary without sanitizers must pass too."""
 import os
@@ -21,7 +21,7 @@ def built():
     return True
 
 
-@pytest.mark.parametrize("binary", ["ga_host_selftest_asan", "ga_host_selftest_tsan", "ga_host_selftest"])
+@pytest.mark.parametrize("binary", ["ga_host_selftest_asan", "ga_host_selftest"])
 def test_host_selftest(built, binary):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1")

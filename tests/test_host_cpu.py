@@ -63,38 +63,6 @@ def test_tiebreak_table_matches_cpython(lib, seed, steps):
         assert state_digest((3, tuple(int(x) for x in out), None)) == state_digest(states[D])
 
 
-@pytest.mark.parametrize("seed,steps,threads", [(3, 5000, 2), (11, 20000, 8), (14, 40961, 4), (6, 9000, 16)])
-def test_tiebreak_table_threaded_matches_cpython(lib, seed, steps, threads):
-    """The threaded table build (ga_rng.h build_rng_threaded, the product's since round 6): the same entries and
-    states as CPython's random.choice draws (the twists sequential, the scan in chunks from speculative start
-    classes)."""
-    lib.ga_debug_rng_threaded.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64, C.c_void_p,
-                                          C.c_void_p]
-    random.seed(seed)
-    for _ in range(seed % 5):
-        random.random()
-    st = np.array(random.getstate()[1], dtype=np.uint32)
-    sizes = [3, 2, 2, 2, 3, 2, 2, 2, 3] * 2
-    want, states = [], [random.getstate()]
-    for _ in range(steps):
-        r = [random.choice(range(s)) for s in sizes]
-        lv = _choice_levels(r)
-        e = 0
-        for half in (0, 1):
-            for S in range(1, 8):
-                e |= lv[half][S] << (2 * S + 1 + 14 * half)
-        want.append(e)
-        states.append(random.getstate())
-    for D in sorted({0, 1, steps // 3, steps}):
-        tab = np.zeros(steps, np.uint32)
-        out = np.zeros(625, np.uint32)
-        ms = C.c_double(0)
-        assert lib.ga_debug_rng_threaded(st.ctypes.data, steps, threads, tab.ctypes.data, D, out.ctypes.data,
-                                         C.byref(ms)) == 0
-        assert tab.tolist() == want
-        assert state_digest((3, tuple(int(x) for x in out), None)) == state_digest(states[D])
-
-
 @pytest.mark.parametrize("seed,steps,chunk", [(2, 5000, 1), (5, 20000, 777), (9, 12000, 4000), (4, 3001, 3001)])
 def test_tiebreak_stream_resumes_exactly(lib, seed, steps, chunk):
     """The resumable table stream (align_many's continuous tie-break table): built in chunks it equals the
