@@ -82,9 +82,9 @@ MULTI_GPU_DEFAULT = "c4"
 # (round 5, tools/profile_r05.sh on the round-5 fills: C3 / C5 / C2 the recompute walk's checkpointing lane fill
 # fill_lane_kernel<4,4,0,16,...,RC,LATE>, C4 the score-only lane fill fill_lane_kernel<4,8,0,16>; the mixes from
 # tools/lane_variant_asm.sh + tools/valu_mix.py --asm-block-with v_min3_i32)
-TRAFFIC_FILES = {w: f"r05/traffic_{w}.json" for w in ("c3", "c4", "c5", "c2")}
-VALU_FILES = {w: f"r05/valu_{w}.json" for w in ("c3", "c4", "c5", "c2")}
-VALU_MIX_FILES = {w: f"r05/valu_mix_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+TRAFFIC_FILES = {w: f"r06/traffic_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+VALU_FILES = {w: f"r06/valu_{w}.json" for w in ("c3", "c4", "c5", "c2")}
+VALU_MIX_FILES = {w: f"r06/valu_mix_{w}.json" for w in ("c3", "c4", "c5", "c2")}
 VALU_RATE_FILE = "r02/valu_rate.txt"
 
 

@@ -236,7 +236,7 @@ def edge_preflight(dist, links, engine, a_codes, b_codes, tables):
     """bench.py --gpus N, before any timed step: load this rank's slab and link its edges (ipc_agreed: every rank
     tries its IPC links, and a failure on any makes all of them use bands), then report, for each slab boundary,
     which GPUs it joins and which transport carries its edge -- so that a fallback is visible in the bench line,
-    not only on stderr.  The first step reuses the links.  Collective over all ranks."""
+    not only on stderr.  Collective over all ranks."""
     rank, world = links.rank, links.world
     edges = slab_bounds(len(b_codes), world)
     engine.load_slab(a_codes, b_codes, tables, edges[rank], edges[rank + 1])
@@ -252,6 +252,8 @@ def edge_preflight(dist, links, engine, a_codes, b_codes, tables):
                                       getattr(pr, "pci_device_id", 0))
         except Exception:  # noqa: BLE001 (diagnostic only)
             pci = None
+    # every step loads its slab again (ga_problem_set_slab drops a context's links): the first step links anew
+    links.ipc_linked_now = False
     info = {"rank": rank, "device": dev, "pci": pci, "ipc_error": links.ipc_error}
     everyone = [None] * world
     dist.all_gather_object(everyone, info, group=links.ctrl)
