@@ -508,12 +508,23 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // Stripes of at most 4 columns per lane (unless GA_LANE_COLS_PER_LANE asks): a block is 64 rows of one stripe, and the walk reads ~1-2 of
         // its TD tiles, so wider blocks starve the walk (C4 on one GPU at TD 8: fill 226 ms, walk 160 ms;
         // at TD 4: 284 + 90 ms, tools/exp/r3b_c4tb3.sh, r3b_c4rc.py)
-        if (c->T > 4 && !c->lane_T_req && !lane_geometry(c, n, &qrows, false, 4, 4))
-            return fail(GA_E_STATE, "recompute fill geometry");
         // and 4 where the geometry model chose fewer (round 4, the lean sub-chunk): fewer, wider stripes shorten
         // the ramp as much as their slower step lengthens the rows, and the walk's blocks come cheaper (C3: fill
-        // 9.69 -> 9.81 ms, walk 5.72 -> 5.42; C5 3.92 against 6.3 ms at TD = 1; tools/r4_td.sh)
-        if (c->T < 4 && !c->lane_T_req) (void)lane_geometry(c, n, &qrows, false, 4, 4);
+        // 9.69 -> 9.81 ms, walk 5.72 -> 5.42; C5 3.92 against 6.3 ms at TD = 1; tools/r4_td.sh).
+        // Round 6: with the lean ramp (the first 64 steps no longer masked) and the cone-shaped recompute window
+        // below, 2 columns per lane win for small alphabets whose stripes all run at once (one workgroup of four per
+        // CU): C3 fill 7.61 -> 6.83 ms, walk 5.18 -> 5.03 (cone 2; 5.65 with the round-5 window), call 12.98 ->
+        // 12.09; C2 1.42 -> 1.30.  The protein fill does not (C5 at TD 2: fill 1.73 -> 1.91 ms), so K > 8 keeps 4
+        // (tools/exp/r6/check5.sh, check6.sh, rc_diag.py).
+        if (!c->lane_T_req) {
+            const bool td2 = c->K <= 8 && (n + 127) / 128 <= 4 * (int64_t)c->num_cu;
+            if (td2 && lane_geometry(c, n, &qrows, false, 2, 4)) {
+            } else if (c->T > 4) {
+                if (!lane_geometry(c, n, &qrows, false, 4, 4)) return fail(GA_E_STATE, "recompute fill geometry");
+            } else if (c->T < 4) {
+                (void)lane_geometry(c, n, &qrows, false, 4, 4);
+            }
+        }
         // The checkpoint spacing, with the stripes' geometry known: the smallest (<= 4096 steps) whose states
         // fit the memory budget (default 96 GB of the 288: C4 on one GPU, TD 4, takes 128 steps, 78 GB; 64
         // would take 156 GB and walks no faster) and whose worker fits LDS; GA_RC_EVERY fixes it (the stripes
@@ -1218,7 +1229,7 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
     {
         // the window: blocks up-left of the walker's (dbi block rows, dbs stripes), the path's likeliest
         // first: it runs near the diagonal, so the key is the tile distance plus the distance off the
-        // diagonal, dbi + dbs*TD + cone*|dbi - dbs*TD| (cone 1 by default; GA_RC_CONE weighs the off-diagonal
+        // diagonal, dbi + dbs*TD + cone*|dbi - dbs*TD| (GA_RC_CONE weighs the off-diagonal
         // distance more, which reaches further along the diagonal with the same 64 blocks).  Only the first
         // nwin are recomputed ahead (the walker's own 2 x 2 tiles always rank first); speculative blocks cost
         // the workers' time and the claims.  Candidates up to 31 block rows / 7 stripes away (offsets dbi*8 + dbs)
@@ -1228,7 +1239,10 @@ int rc_walk_launch(ga_ctx* c, int64_t ntab, const WalkStart& st, WalkBufs& wb) {
         // blocks in all three).
         const int span = c->knob("GA_RC_SPAN") ? std::max(2, std::min(ga::RC_SPAN_I, atoi(c->knob("GA_RC_SPAN"))))
                                                : ga::RC_SPAN_I;
-        const int cone = c->knob("GA_RC_CONE") ? std::max(1, std::min(8, atoi(c->knob("GA_RC_CONE")))) : 1;
+        // (cone 3 by default since round 6: the same 64 candidates reach further along the diagonal, so the walker
+        // waits less on its tiles (C3 tile waits 0.31 -> 0.15 ms at TD 4, 0.70 -> 0.14 at TD 2) with fewer blocks
+        // recomputed (TD 2: 16.7k -> 12.5k); cones 2 and 4 walk as fast, tools/exp/r6/check6.sh)
+        const int cone = c->knob("GA_RC_CONE") ? std::max(1, std::min(8, atoi(c->knob("GA_RC_CONE")))) : 3;
         std::vector<std::pair<int, int>> off;
         for (int di = 0; di < span; di++)
             for (int dj = 0; dj < std::min(span, ga::RC_SPAN_S); dj++)

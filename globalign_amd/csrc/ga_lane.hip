@@ -454,9 +454,10 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
     // the lean steady state's checkpoint store: a raw buffer over the stripe's rows (base and size in SGPRs) and a
     // 32-bit offset per lane, rows rlo + lane - 48 for lanes 48..63 (LEAN sub-chunks hold no row past m), off the
     // buffer's end for the others, whose stores the buffer's range check then drops: no exec change, and no scratch
-    // writes (they were three quarters of the store's bytes); off = cb + cm * rlo
+    // writes (they were three quarters of the store's bytes); off = cb + 8 rlo for every lane, one v_add with an
+    // SGPR (a per-lane multiplier took a 64-bit v_mad_u64_u32): the other lanes' 0x7ffffff0 + 8 rlo stays past
+    // the buffer's (m + 1) * 8 bytes and below 2^32 while rc_rows_fit(m) (ga_check.h), which the host requires
     const unsigned ck_cb = lane >= 48 ? (unsigned)(lane - 48) * 8u : 0x7ffffff0u;
-    const unsigned ck_cm = lane >= 48 ? 8u : 0u;
     lk_v4i ck_rsrc = {0, 0, 0, 0};
     if (RC && p.colck != nullptr) {
         const unsigned long long cbase = reinterpret_cast<unsigned long long>(colck_s);
@@ -723,7 +724,7 @@ __global__ void __launch_bounds__(lane_block_threads(NWC)) fill_lane_kernel(Fill
                     if (RC && LEAN) {
                         // (colck is set whenever the RC variant runs, enqueue_fill) one offset and one store
                         const lk_v2u vv = (lane & 4) ? lk_v2u{(unsigned)R[0], (unsigned)R[1]} : lk_v2u{(unsigned)R[2], (unsigned)R[3]};
-                        const unsigned off = ck_cb + ck_cm * (unsigned)rlo;
+                        const unsigned off = ck_cb + sgpr_u(8u * (unsigned)rlo);
                         asm volatile("buffer_store_dwordx2 %1, %0, %2, 0 offen" ::"v"(off), "v"(vv), "s"(ck_rsrc) : "memory");
                     } else if (RC && p.colck != nullptr) {
                         // lanes 48..63 hold rows rlo .. rlo+15 of the stripe's right edge; every lane stores (lanes
