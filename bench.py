@@ -29,6 +29,7 @@ are visible (GA_DIST_BACKEND=gloo rehearses the ranks without that check).
 import argparse
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -192,7 +193,15 @@ def golden_cost(workload):
     return json.load(open(path)).get("cost")
 
 
-def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None):
+def _variant_td(name):
+    """Columns per lane (the second template argument) of a fill_lane_kernel name or mangled symbol, else None."""
+    if not name:
+        return None
+    m = re.search(r"fill_lane_kernel<\s*\d+\s*,\s*(\d+)", name) or re.search(r"fill_lane_kernelILi\d+ELi(\d+)E", name)
+    return int(m.group(1)) if m else None
+
+
+def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None, fill_kind=None):
     """What bounds the fill, from the committed profiles.
 
     The row-scan fill keeps M/X/Y in registers and LDS: it moves ~1 B/cell (PMC FETCH+WRITE), not the
@@ -219,6 +228,14 @@ def roofline(workload, wl, fill_ms, per_step_ms=None, profile_cells=None):
                    "frac": hbm_alg / HBM_PEAK_GBS,
                    "measured_GBps": traffic / secs / 1e9 if traffic else None,
                    "measured_bytes_per_cell": traffic / cells if traffic else None}}
+    # the committed profiles must be of the kernel variant that ran (columns per lane): a default that changed after
+    # the last profile run would otherwise divide one variant's instructions by another's time
+    run_td = fill_kind[1] if fill_kind and fill_kind[0] in ("lane", "rc") else None
+    prof_tds = {_variant_td(_profile(VALU_FILES.get(workload, ""), "kernel")), _variant_td((mix or {}).get("symbol"))}
+    if run_td is not None and prof_tds != {run_td}:
+        out["profile_mismatch"] = (f"the committed profiles are of {sorted(t for t in prof_tds if t)} columns per lane, "
+                                   f"this fill ran {run_td}: achieved left null until tools/profile_r06.sh is re-run")
+        insts = None
     if insts and mix:
         peak = mix["peak_valu_insts_per_s"]
         rate = insts / secs
@@ -361,7 +378,7 @@ def single_line(args, workload, wl):
         "config": {"workload": wl["desc"], "m": wl["m"], "n": wl["n"], "traceback": wl["traceback"],
                    "parallelism": "single GPU", "cost": r["cost"], "oracle_cost": gold,
                    "cost_matches_oracle": (r["cost"] == gold) if gold is not None else None},
-        "roofline": roofline(workload, wl, r["fill_ms"]),
+        "roofline": roofline(workload, wl, r["fill_ms"], fill_kind=r.get("fill_kind")),
         "fill_ms": r["fill_ms"],
         "fill_cells_per_s": r["cells"] / (r["fill_ms"] * 1e-3),
     }
@@ -390,7 +407,7 @@ def single_line(args, workload, wl):
         g4 = golden_cost("c4")
         line["c4"] = {"workload": w4["desc"], "value": h["value"], "unit": "cells/s", "n_gpus": 1,
                       "ms_per_step": h["ms_per_step"], "cost": h["cost"], "cost_matches_oracle": h["cost"] == g4,
-                      "fill_ms": h["fill_ms"], "roofline": roofline("c4", w4, h["fill_ms"])}
+                      "fill_ms": h["fill_ms"], "roofline": roofline("c4", w4, h["fill_ms"], fill_kind=h.get("fill_kind"))}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     print(json.dumps(line), flush=True)

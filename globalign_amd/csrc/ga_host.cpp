@@ -515,9 +515,11 @@ int enqueue_fill(ga_ctx* c, int32_t flags, const Band& bd = Band()) {
         // below, 2 columns per lane win for small alphabets whose stripes all run at once (one workgroup of four per
         // CU): C3 fill 7.61 -> 6.83 ms, walk 5.18 -> 5.03 (cone 2; 5.65 with the round-5 window), call 12.98 ->
         // 12.09; C2 1.42 -> 1.30.  The protein fill does not (C5 at TD 2: fill 1.73 -> 1.91 ms), so K > 8 keeps 4
-        // (tools/exp/r6/check5.sh, check6.sh, rc_diag.py).
+        // (tools/exp/r6/check5.sh, check6.sh, rc_diag.py).  Behind the option GA_RC_NARROW=1 until the GPU suite has
+        // run with it as the default and the roofline profiles are of that variant.
         if (!c->lane_T_req) {
-            const bool td2 = c->K <= 8 && (n + 127) / 128 <= 4 * (int64_t)c->num_cu;
+            const char* nw = c->knob("GA_RC_NARROW");
+            const bool td2 = nw && atoi(nw) && !c->slab && c->K <= 8 && (n + 127) / 128 <= 4 * (int64_t)c->num_cu;
             if (td2 && lane_geometry(c, n, &qrows, false, 2, 4)) {
             } else if (c->T > 4) {
                 if (!lane_geometry(c, n, &qrows, false, 4, 4)) return fail(GA_E_STATE, "recompute fill geometry");

@@ -92,19 +92,19 @@ def test_rc_checkpoint_spacing_vs_oracle(monkeypatch, every):
     _align(monkeypatch, splitmix_seq(3000, 31, "dna"), splitmix_seq(3500, 32, "dna"), DNA, seed=every, env={"GA_RC_EVERY": every})
 
 
-@pytest.mark.parametrize("td", [None, 4])
+@pytest.mark.parametrize("td", ["narrow", 4])
 @pytest.mark.parametrize("env", [{"GA_RC_SERVERS": 1, "GA_RC_WIN": 4},
                                  {"GA_RC_SERVERS": 2, "GA_RC_WIN": 64, "GA_RC_WPW": 6},
                                  {"GA_RC_SERVERS": 160, "GA_RC_WPW": 4},
                                  {"GA_RC_SERVERS": 1, "GA_RC_WIN": 4, "GA_RC_CONE": 1}])
 def test_rc_worker_pools_vs_oracle(monkeypatch, env, td):
-    """One worker behind a narrow window, a few many-worker groups, many groups racing for claims, at the default
-    stripe width for DNA (2 columns per lane since round 6) and at 4: the window always offers the walker's own
+    """One worker behind a narrow window, a few many-worker groups, many groups racing for claims, at 2 columns per
+    lane (GA_RC_NARROW's choice for DNA) and at 4: the window always offers the walker's own
     2 x 2 blocks first, so even one worker behind a 4-block window never starves it of the stripe to its left (round
     4 kept this case at TD < 4), whatever the cone that ranks the rest."""
-    env = dict(env) if td is None else dict(env, GA_LANE_COLS_PER_LANE=td)
+    env = dict(env, GA_RC_NARROW=1) if td == "narrow" else dict(env, GA_LANE_COLS_PER_LANE=td)
     kind = _align(monkeypatch, splitmix_seq(2500, 41, "dna"), splitmix_seq(2600, 42, "dna"), DNA, seed=7, env=env)
-    assert kind[1] == (td or 2), kind
+    assert kind[1] == (2 if td == "narrow" else td), kind
 
 
 @pytest.mark.parametrize("jump", [0, pytest.param(1, marks=needs_jump)])
