@@ -54,3 +54,18 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "c1"],
                        env=dict(os.environ, PYTHONPATH=ROOT, **e), capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "launcher started 1 ranks" in r.stderr
+
+
+def test_roofline_profiles_must_match_the_variant_that_ran():
+    """bench.roofline divides the committed profile's SQ_INSTS_VALU per launch by the fill's measured time: only when
+    the profile (and its VALU mix) are of the kernel variant that ran (columns per lane), else achieved stays null."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench._variant_td("void ga::fill_lane_kernel<4, 2, 0, 16, false, false, true, true>(ga::FillArgs)") == 2
+    assert bench._variant_td("_ZN2ga16fill_lane_kernelILi4ELi8ELi0ELi16ELb0ELb0ELb0ELb0EEEvNS_8FillArgsE") == 8
+    assert bench._variant_td("fill_kernel") is None
+    c3 = bench.WORKLOADS["c3"]
+    ok = bench.roofline("c3", c3, 7.6, fill_kind=("rc", 4, 391, 4, 98))
+    assert "profile_mismatch" not in ok and 0 < ok["frac"] < 1
+    bad = bench.roofline("c3", c3, 6.8, fill_kind=("rc", 2, 782, 4, 196))
+    assert bad["achieved"] is None and bad["frac"] is None and "profile_mismatch" in bad
