@@ -246,4 +246,6 @@ struct LaneSub;
 
 if __name__ == "__main__":
     import sys
+    if len(sys.argv) > 1 and sys.argv[1].startswith("-"):
+        sys.exit(__doc__)  # (an option is not an output path)
     main(sys.argv[1] if len(sys.argv) > 1 else OUT)
